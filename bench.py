@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: "GiB/s device-resident split+ref-hash; chunk/ref bit-parity
+vs Go ref".
+
+Workload (BASELINE.json configs[1], and configs[3] when launched on 8 GPUs): one 1 GiB random
+byte stream per GPU (SplitMix64 counter stream generated in HBM, seed 0xB5B52026 + rank),
+split.NewWriter defaults (Bits 16, MinSize 1024). A step = one full pass of the hot path over
+that stream: rolling-hash scan -> MinSize boundary selection -> SHA-256 of every chunk, with the
+(offset, len, level, ref) records left in HBM. Streams are independent: no collectives on the
+data path (weak scaling); torch.distributed is used only for the barrier and the max-over-ranks
+timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "GiB/s device-resident split+ref-hash; chunk/ref bit-parity vs Go ref"
+BASE_SEED = 0xB5B52026
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--stream-mib", type=int, default=1024, help="bytes per stream (MiB)")
+    ap.add_argument("--streams", type=int, default=1, help="independent streams per GPU")
+    ap.add_argument("--bits", type=int, default=16)
+    ap.add_argument("--min-size", type=int, default=1024)
+    ap.add_argument("--cpu-sample-mib", type=int, default=1024,
+                    help="bytes of stream 0 the CPU oracle baseline splits+hashes (0: skip)")
+    ap.add_argument("--check", action="store_true",
+                    help="verify the device records against the CPU oracle after timing")
+    return ap.parse_args()
+
+
+def dist_setup():
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_steps(step, sync, world: int, steps: int, warmup: int) -> float:
+    """W untimed warmups, then exactly K steps between barrier+sync brackets; max over ranks."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier(world)
+    t1 = time.perf_counter()
+    return max_over_ranks(t1 - t0, world)
+
+
+def cpu_baseline(sample_mib: int, bits: int, min_size: int) -> dict | None:
+    """The C oracle ("port" of the reference's per-stream Splitter + sha256) on this host,
+    one thread (the reference runs one goroutine per stream), over the first sample_mib MiB of
+    stream 0."""
+    if sample_mib <= 0:
+        return None
+    from bs_amd.synth import splitmix_array
+    from oracle import oracle as O  # checker / baseline only
+    n = sample_mib << 20
+    data = splitmix_array(BASE_SEED, n)
+    table = O.buzhash32_table(1)
+    t0 = time.perf_counter()
+    ch = O.split(table, data, bits=bits, min_size=min_size)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample_mib} MiB of stream 0 (same bytes/params), C oracle "
+                      f"split+sha256, 1 thread, {len(ch)} chunks in {dt:.2f}s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup()
+    import torch
+    from bs_amd import build, bsgpu
+
+    build.build()
+    assert torch.cuda.is_available(), "bench.py needs a GPU (the HIP path is the product)"
+    torch.cuda.set_device(local)
+    nbytes = args.stream_mib << 20
+    ns = args.streams
+    stride = (nbytes + 15) & ~15
+    buf = torch.empty(stride * ns, dtype=torch.uint8, device=f"cuda:{local}")
+    eng = bsgpu.Engine(device=local)
+    eng.profile(True)
+    offs = [i * stride for i in range(ns)]
+    lens = [nbytes] * ns
+    for i in range(ns):  # stream s of rank r uses seed BASE + r*ns + s
+        bsgpu.fill_splitmix(buf.data_ptr() + offs[i], nbytes, BASE_SEED + rank * ns + i,
+                            stream=eng.stream, device=local)
+    stage_sum = [0.0, 0.0, 0.0]
+    nsteps = [0]
+
+    def step():
+        eng.run(buf.data_ptr(), offs, lens, bits=args.bits, min_size=args.min_size)
+        eng.finish()  # waits on the engine's stream; records stay in HBM
+        ms = eng.stage_ms()
+        for i in range(3):
+            stage_sum[i] += ms[i]
+        nsteps[0] += 1
+
+    def sync():
+        torch.cuda.synchronize(local)
+
+    # warmup steps are counted into stage_sum too; reset after them
+    for _ in range(args.warmup):
+        step()
+    stage_sum[:] = [0.0, 0.0, 0.0]
+    nsteps[0] = 0
+    elapsed = timed_steps(step, sync, world, args.steps, 0)
+    total_bytes = world * ns * nbytes * args.steps
+    value = total_bytes / elapsed / 2**30
+    stage_avg = [s / max(nsteps[0], 1) for s in stage_sum]
+    names = ["k_scan", "k_compact+k_select+k_chunks+prefix", "k_sha"]
+    dom = max(range(3), key=lambda i: stage_avg[i])
+    per_launch_bytes = ns * nbytes  # algorithmic: every input byte read once by the kernel
+    achieved = per_launch_bytes / (stage_avg[dom] * 1e-3) / 1e9 if stage_avg[dom] > 0 else 0.0
+    chunks = eng.nchunks
+    check = None
+    if args.check and rank == 0:
+        from bs_amd.synth import splitmix_array
+        from oracle import oracle as O
+        ref = O.split(O.buzhash32_table(1), splitmix_array(BASE_SEED, nbytes), bits=args.bits,
+                      min_size=args.min_size)
+        got = eng.chunks()[: len(ref)] if ns == 1 else eng.chunks()[: eng.counts()[0]]
+        check = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
+                     and (got["offset"] == ref["offset"]).all())
+    cpu = cpu_baseline(args.cpu_sample_mib, args.bits, args.min_size) \
+        if (rank == 0 and world == 1) else None
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: SplitMix64 counter stream in HBM, seed 0xB5B52026+stream",
+            "config": {"workload": ("configs[1]: 1 GiB random stream per GPU, default split params"
+                                    if (ns == 1 and nbytes == 1 << 30) else
+                                    f"{ns} x {args.stream_mib} MiB streams per GPU"),
+                       "stream_bytes": nbytes, "streams_per_gpu": ns,
+                       "split_bits": args.bits, "min_size": args.min_size, "fanout": 8,
+                       "parallelism": "independent streams, one set per GPU, no collectives"},
+            "roofline": {"bound": "hbm", "kernel": names[dom],
+                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+            "cpu_baseline": cpu,
+            "stage_ms": {n: round(v, 4) for n, v in zip(names, stage_avg)},
+            "chunks_per_step": int(chunks),
+        }
+        if check is not None:
+            line["oracle_check"] = check
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,283 @@
+"""Python binding of libbsgpu (include/bsgpu.h) via ctypes.
+
+This is plumbing for tests and bench.py; it carries no compute of its own. Every function
+runs on the HIP path and raises if the shared library is missing or a call fails — there is no
+CPU fallback anywhere in bs_amd.
+
+Reference surface mirrored: split.NewWriter / Write / Close / Root options Bits, MinSize,
+Fanout (/root/reference/split/split.go:44-165) and bs.Blob.Ref (/root/reference/bs.go:24-26).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbsgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bsgpu.h")
+
+BSG_OK = 0
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EDEVICE", -71: "ESTATE", -19: "ENODEV"}
+
+
+class BsgError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: bsgpu error {code} ({ERRORS.get(code, '?')})")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("split_bits", ctypes.c_uint32), ("min_size", ctypes.c_uint32),
+                ("fanout", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+CHUNK_DTYPE = np.dtype(
+    [("offset", "<u8"), ("len", "<u8"), ("level", "<u4"), ("stream", "<u4"), ("ref", "u1", (32,))]
+)
+assert CHUNK_DTYPE.itemsize == 56
+
+_lib = None
+
+
+def exported_symbols_from_header(path: str = HEADER_PATH) -> list[str]:
+    """Every function name declared in include/bsgpu.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(bsg_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbsgpu.so (built by `python -m bs_amd.build`). Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `python -m bs_amd.build` "
+                           "(the HIP path is the only path; there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8p, u32p, u64p = (ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8),
+                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint64))
+    sig = {
+        "bsg_errstr": (ctypes.c_char_p, [ctypes.c_int]),
+        "bsg_params_default": (Params, []),
+        "bsg_default_table": (None, [u32p]),
+        "bsg_device_count": (ctypes.c_int, []),
+        "bsg_open": (vp, [ctypes.c_int, ctypes.POINTER(Params), u32p, ctypes.POINTER(ctypes.c_int)]),
+        "bsg_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
+        "bsg_close": (ctypes.c_int, [vp]),
+        "bsg_pending": (ctypes.c_size_t, [vp]),
+        "bsg_drain": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
+        "bsg_set_tile": (ctypes.c_int, [vp, ctypes.c_size_t]),
+        "bsg_free": (None, [vp]),
+        "bsg_engine_create": (vp, [ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_int)]),
+        "bsg_engine_destroy": (None, [vp]),
+        "bsg_engine_run": (ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint32,
+                                          ctypes.POINTER(Params)]),
+        "bsg_engine_finish": (ctypes.c_int, [vp, u64p]),
+        "bsg_engine_chunks_device": (vp, [vp]),
+        "bsg_engine_copy_chunks": (ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+        "bsg_engine_copy_counts": (ctypes.c_int, [vp, u64p, ctypes.c_uint32]),
+        "bsg_engine_stream": (vp, [vp]),
+        "bsg_engine_candidates": (ctypes.c_uint64, [vp]),
+        "bsg_engine_profile": (ctypes.c_int, [vp, ctypes.c_int]),
+        "bsg_engine_stage_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
+        "bsg_split_hash_batch": (ctypes.c_int, [ctypes.c_int, vp, u64p, u64p, ctypes.c_uint32,
+                                                ctypes.POINTER(Params), u32p, vp,
+                                                ctypes.c_uint64, u64p, u64p]),
+        "bsg_sha256_batch": (ctypes.c_int, [ctypes.c_int, vp, u64p, u64p, ctypes.c_uint32, vp]),
+        "bsg_fill_splitmix": (ctypes.c_int, [ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64,
+                                             vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != BSG_OK:
+        raise BsgError(rc, what)
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+def _p(a: np.ndarray, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def device_count() -> int:
+    return lib().bsg_device_count()
+
+
+def default_table() -> np.ndarray:
+    t = np.zeros(256, dtype=np.uint32)
+    lib().bsg_default_table(_p(t, ctypes.c_uint32))
+    return t
+
+
+def params(bits: int = 16, min_size: int = 1024, fanout: int = 8) -> Params:
+    """split.NewWriter defaults (split/split.go:48,88-89); pass Bits/MinSize/Fanout overrides."""
+    return Params(bits, min_size, fanout, 0)
+
+
+def _table_arg(table):
+    if table is None:
+        return None, None
+    t = np.ascontiguousarray(np.asarray(table, dtype=np.uint32))
+    assert t.shape == (256,)
+    return t, _p(t, ctypes.c_uint32)
+
+
+def split_hash_batch(streams: list[bytes] | list[np.ndarray], bits: int = 16,
+                     min_size: int = 1024, table=None, device: int = 0):
+    """Split + hash host-resident streams on the GPU. Returns (chunks, counts)."""
+    arrs = [np.frombuffer(bytes(s), dtype=np.uint8) if not isinstance(s, np.ndarray)
+            else np.ascontiguousarray(s, dtype=np.uint8) for s in streams]
+    lens = _u64([len(a) for a in arrs])
+    off = _u64(np.concatenate([[0], np.cumsum(lens)[:-1]]) if len(arrs) else [])
+    base = np.concatenate(arrs) if arrs else np.zeros(1, np.uint8)
+    if base.size == 0:
+        base = np.zeros(1, np.uint8)
+    cap = int(sum(int(l) // min_size + 2 for l in lens)) + 1
+    out = np.zeros(cap, dtype=CHUNK_DTYPE)
+    counts = np.zeros(max(len(arrs), 1), dtype=np.uint64)
+    n = ctypes.c_uint64(0)
+    p = params(bits, min_size)
+    _t, tp = _table_arg(table)
+    rc = lib().bsg_split_hash_batch(device, base.ctypes.data, _p(off, ctypes.c_uint64),
+                                    _p(lens, ctypes.c_uint64), len(arrs), ctypes.byref(p), tp,
+                                    out.ctypes.data, cap, _p(counts, ctypes.c_uint64),
+                                    ctypes.byref(n))
+    _check(rc, "bsg_split_hash_batch")
+    return out[: n.value], counts[: len(arrs)]
+
+
+def sha256_batch(blobs: list[bytes], device: int = 0) -> list[bytes]:
+    arrs = [np.frombuffer(bytes(b), dtype=np.uint8) for b in blobs]
+    lens = _u64([len(a) for a in arrs])
+    off = _u64(np.concatenate([[0], np.cumsum(lens)[:-1]]) if arrs else [])
+    base = np.concatenate(arrs) if arrs else np.zeros(1, np.uint8)
+    if base.size == 0:
+        base = np.zeros(1, np.uint8)
+    refs = np.zeros(32 * max(len(arrs), 1), dtype=np.uint8)
+    rc = lib().bsg_sha256_batch(device, base.ctypes.data, _p(off, ctypes.c_uint64),
+                                _p(lens, ctypes.c_uint64), len(arrs), refs.ctypes.data)
+    _check(rc, "bsg_sha256_batch")
+    return [refs[32 * i:32 * i + 32].tobytes() for i in range(len(arrs))]
+
+
+def fill_splitmix(ptr: int, nbytes: int, seed: int, stream: int | None = None,
+                  device: int = 0) -> None:
+    _check(lib().bsg_fill_splitmix(device, ptr, nbytes, seed, stream), "bsg_fill_splitmix")
+
+
+class Engine:
+    """Device-resident batch of independent streams (bsg_engine_*)."""
+
+    def __init__(self, device: int = 0, table=None):
+        err = ctypes.c_int(0)
+        self._t, tp = _table_arg(table)
+        self.h = lib().bsg_engine_create(device, tp, ctypes.byref(err))
+        if not self.h:
+            raise BsgError(err.value, "bsg_engine_create")
+        self.nstreams = 0
+
+    def run(self, d_ptr: int, off, lens, bits: int = 16, min_size: int = 1024) -> None:
+        self._off, self._len = _u64(off), _u64(lens)
+        self._p = params(bits, min_size)
+        self.nstreams = len(self._off)
+        _check(lib().bsg_engine_run(self.h, d_ptr, _p(self._off, ctypes.c_uint64),
+                                    _p(self._len, ctypes.c_uint64), self.nstreams,
+                                    ctypes.byref(self._p)), "bsg_engine_run")
+
+    def finish(self) -> int:
+        n = ctypes.c_uint64(0)
+        _check(lib().bsg_engine_finish(self.h, ctypes.byref(n)), "bsg_engine_finish")
+        self.nchunks = n.value
+        return n.value
+
+    def chunks(self) -> np.ndarray:
+        out = np.zeros(max(self.nchunks, 1), dtype=CHUNK_DTYPE)
+        _check(lib().bsg_engine_copy_chunks(self.h, out.ctypes.data, self.nchunks),
+               "bsg_engine_copy_chunks")
+        return out[: self.nchunks]
+
+    def counts(self) -> np.ndarray:
+        c = np.zeros(max(self.nstreams, 1), dtype=np.uint64)
+        _check(lib().bsg_engine_copy_counts(self.h, _p(c, ctypes.c_uint64), self.nstreams),
+               "bsg_engine_copy_counts")
+        return c[: self.nstreams]
+
+    @property
+    def stream(self) -> int:
+        return lib().bsg_engine_stream(self.h) or 0
+
+    def profile(self, enable: bool = True) -> None:
+        _check(lib().bsg_engine_profile(self.h, int(enable)), "bsg_engine_profile")
+
+    def stage_ms(self) -> list[float]:
+        out = (ctypes.c_float * 3)()
+        _check(lib().bsg_engine_stage_ms(self.h, out), "bsg_engine_stage_ms")
+        return [float(x) for x in out]
+
+    @property
+    def candidates(self) -> int:
+        return lib().bsg_engine_candidates(self.h)
+
+    def close(self) -> None:
+        if self.h:
+            lib().bsg_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class StreamingSplitter:
+    """bsg_open/bsg_write/bsg_close/bsg_drain: the C-ABI form of split.Writer's chunking."""
+
+    def __init__(self, bits: int = 16, min_size: int = 1024, fanout: int = 8, table=None,
+                 device: int = 0, tile: int | None = None):
+        err = ctypes.c_int(0)
+        self._p = params(bits, min_size, fanout)
+        self._t, tp = _table_arg(table)
+        self.h = lib().bsg_open(device, ctypes.byref(self._p), tp, ctypes.byref(err))
+        if not self.h:
+            raise BsgError(err.value, "bsg_open")
+        if tile is not None:
+            _check(lib().bsg_set_tile(self.h, tile), "bsg_set_tile")
+
+    def write(self, data) -> int:
+        b = bytes(data)
+        _check(lib().bsg_write(self.h, b, len(b)), "bsg_write")
+        return len(b)
+
+    def close(self) -> None:
+        _check(lib().bsg_close(self.h), "bsg_close")
+
+    def drain(self) -> np.ndarray:
+        n = lib().bsg_pending(self.h)
+        out = np.zeros(max(n, 1), dtype=CHUNK_DTYPE)
+        got = lib().bsg_drain(self.h, out.ctypes.data, n)
+        return out[:got]
+
+    def free(self) -> None:
+        if self.h:
+            lib().bsg_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

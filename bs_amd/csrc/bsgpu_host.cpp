@@ -1,0 +1,703 @@
+// bsgpu_host.cpp — libbsgpu host side: device workspaces, the run pipeline and the C ABI
+// declared in include/bsgpu.h.
+//
+// A run = one launch sequence over a batch of stream segments (bsgpu_internal.h):
+//   memset(counters) → k_init → k_scan → prefix(strip counts) → k_compact → k_select
+//   → prefix(flags) → k_chunks → k_sha
+// Everything after k_scan sizes itself from device-side counters, so a run never waits on the
+// host; bsg_engine_finish() is the only synchronisation (and the place where a too-small
+// candidate buffer is grown and the run repeated).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <vector>
+
+#include "../../include/bsgpu.h"
+#include "bsgpu_internal.h"
+#include "bsgpu_launch.h"
+#include "buzhash32_table.inc"
+
+using namespace bsg;
+
+namespace {
+
+const uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                         0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 8;  // headroom against regrowth
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipMalloc(&p, bytes);
+      if (e != hipSuccess) return e;
+      want = bytes;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    cap = bytes;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+int herr(hipError_t e) { return e == hipSuccess ? BSG_OK : BSG_EDEVICE; }
+
+#define HCHECK(x)                           \
+  do {                                      \
+    hipError_t e_ = (x);                    \
+    if (e_ != hipSuccess) {                 \
+      (void)hipGetLastError();              \
+      return BSG_EDEVICE;                   \
+    }                                       \
+  } while (0)
+
+int normalize(const bsg_params* in, Params* out, bsg_params* norm) {
+  bsg_params p = in ? *in : bsg_params_default();
+  if (p.split_bits == 0) p.split_bits = 13;  // hashsplit defaultSplitBits
+  if (p.min_size == 0) p.min_size = 64;      // hashsplit defaultMinSize (window size)
+  if (p.fanout == 0) p.fanout = 8;
+  if (p.split_bits > 32 || p.min_size < 64) return BSG_EINVAL;
+  out->split_bits = p.split_bits;
+  out->min_size = p.min_size;
+  out->mask = p.split_bits >= 32 ? 0xffffffffu : ((1u << p.split_bits) - 1u);
+  out->pad_ = 0;
+  if (norm) *norm = p;
+  return BSG_OK;
+}
+
+}  // namespace
+
+struct bsg_engine {
+  int dev = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  DevBuf table, streams, strip0, counts, slots, strip_off, partials_a, partials_b, cand, flags,
+      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr;
+  PinBuf h_streams, h_strip0, h_ctr;
+  // current run
+  const uint8_t* d_data = nullptr;
+  std::vector<StreamDesc> descs;
+  Params p{};
+  uint64_t nstrips = 0, cand_cap = 0, chunk_cap = 0;
+  uint64_t retry_cap = 0;  // exact candidate capacity after an overflow (one re-run)
+  uint32_t nstreams = 0;
+  bool enqueued = false;
+  Counters last{};
+  // optional per-stage HIP events on the engine stream: [scan, compact..chunks, sha]
+  bool profile = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  float stage_ms[3] = {0, 0, 0};
+
+  void mark(int i) {
+    if (profile && ev[i]) (void)hipEventRecord(ev[i], stream);
+  }
+
+  int setdev() { return herr(hipSetDevice(dev)); }
+
+  int enqueue() {
+    const uint32_t ns = nstreams;
+    // strips
+    std::vector<uint64_t> s0(ns + 1);
+    uint64_t strips = 0, total_len = 0, chunk_bound = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+      descs[s].strip0 = strips;
+      s0[s] = strips;
+      strips += (descs[s].len + kStrip - 1) / kStrip;
+      total_len += descs[s].len;
+      chunk_bound += (descs[s].len + (descs[s].seg_base - descs[s].open_start)) / p.min_size + 2;
+    }
+    s0[ns] = strips;
+    nstrips = strips;
+    chunk_cap = chunk_bound;
+    {
+      // random input yields ~len/2^bits candidates; degenerate input (e.g. all zeros: one per
+      // byte) overflows this estimate and is re-run once at its exact size by finish().
+      const uint32_t b = std::min<uint32_t>(p.split_bits, 16);
+      cand_cap = std::max<uint64_t>(1u << 16, ((total_len >> b) << 2) + 2ull * ns + 1024);
+      if (retry_cap > cand_cap) cand_cap = retry_cap;
+    }
+    HCHECK(streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
+    HCHECK(strip0.ensure(sizeof(uint64_t) * (ns + 1)));
+    HCHECK(counts.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
+    HCHECK(slots.ensure(sizeof(uint32_t) * kSlotCap * (strips ? strips : 1)));
+    HCHECK(strip_off.ensure(sizeof(uint64_t) * (strips ? strips : 1)));
+    HCHECK(partials_a.ensure(sizeof(uint64_t) * prefix_partials_needed(strips)));
+    HCHECK(partials_b.ensure(sizeof(uint64_t) * prefix_partials_needed(cand_cap)));
+    HCHECK(cand.ensure(sizeof(uint64_t) * cand_cap));
+    HCHECK(flags.ensure(sizeof(uint32_t) * cand_cap));
+    HCHECK(fidx.ensure(sizeof(uint64_t) * cand_cap));
+    HCHECK(bnd_end.ensure(sizeof(uint64_t) * chunk_cap));
+    HCHECK(bnd_info.ensure(sizeof(uint64_t) * chunk_cap));
+    HCHECK(out.ensure(sizeof(ChunkRec) * chunk_cap));
+    HCHECK(scount.ensure(sizeof(uint64_t) * (ns ? ns : 1)));
+    HCHECK(last_end.ensure(sizeof(uint64_t) * (ns ? ns : 1)));
+    HCHECK(carry.ensure(sizeof(CarryOut) * (ns ? ns : 1)));
+    HCHECK(ctr.ensure(sizeof(Counters)));
+    HCHECK(h_streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
+    HCHECK(h_strip0.ensure(sizeof(uint64_t) * (ns + 1)));
+    HCHECK(h_ctr.ensure(sizeof(Counters)));
+
+    // The pinned staging of the previous run may still be in flight: finish() synchronised.
+    std::memcpy(h_streams.p, descs.data(), sizeof(StreamDesc) * ns);
+    std::memcpy(h_strip0.p, s0.data(), sizeof(uint64_t) * (ns + 1));
+    HCHECK(hipMemcpyAsync(streams.p, h_streams.p, sizeof(StreamDesc) * ns, hipMemcpyHostToDevice,
+                          stream));
+    HCHECK(hipMemcpyAsync(strip0.p, h_strip0.p, sizeof(uint64_t) * (ns + 1),
+                          hipMemcpyHostToDevice, stream));
+    HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
+    Counters* dctr = ctr.as<Counters>();
+
+    InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
+                carry.as<CarryOut>()};
+    if (ns) HCHECK(launch_init(ia, stream));
+
+    ScanArgs sa{};
+    sa.data = d_data;
+    sa.streams = streams.as<StreamDesc>();
+    sa.strip0 = strip0.as<uint64_t>();
+    sa.nstreams = ns;
+    sa.nstrips = strips;
+    sa.table = table.as<uint32_t>();
+    sa.p = p;
+    sa.counts = counts.as<uint32_t>();
+    sa.slots = slots.as<uint32_t>();
+    sa.cand_off = strip_off.as<uint64_t>();
+    sa.cand = cand.as<uint64_t>();
+    sa.cand_cap = cand_cap;
+    sa.ctr = dctr;
+    mark(0);
+    if (strips) HCHECK(launch_scan(sa, stream, num_cus));
+    mark(1);
+
+    PrefixArgs pa{};
+    pa.in = counts.as<uint32_t>();
+    pa.out = strip_off.as<uint64_t>();
+    pa.partials = partials_a.as<uint64_t>();
+    pa.n_bound = strips;
+    pa.n_dev = nullptr;
+    pa.total = &dctr->ncand;
+    pa.overflow = &dctr->overflow;
+    pa.cap = cand_cap;
+    pa.skip_if = nullptr;
+    HCHECK(launch_prefix(pa, stream));
+
+    if (strips) HCHECK(launch_compact(sa, stream, num_cus));
+
+    SelArgs sel{cand.as<uint64_t>(), streams.as<StreamDesc>(), flags.as<uint32_t>(), p, dctr};
+    HCHECK(launch_select(sel, cand_cap, stream, num_cus));
+
+    PrefixArgs pf{};
+    pf.in = flags.as<uint32_t>();
+    pf.out = fidx.as<uint64_t>();
+    pf.partials = partials_b.as<uint64_t>();
+    pf.n_bound = cand_cap;
+    pf.n_dev = &dctr->ncand;
+    pf.total = &dctr->nchunks;
+    pf.overflow = nullptr;
+    pf.cap = 0;
+    pf.skip_if = &dctr->overflow;
+    HCHECK(launch_prefix(pf, stream));
+
+    ChunkArgs ca{cand.as<uint64_t>(), flags.as<uint32_t>(), fidx.as<uint64_t>(),
+                 bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
+                 last_end.as<uint64_t>(), chunk_cap, p, dctr};
+    HCHECK(launch_chunks(ca, cand_cap, stream, num_cus));
+
+    ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
+               bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
+               carry.as<CarryOut>(), chunk_cap};
+    mark(2);
+    HCHECK(launch_sha(sh, chunk_cap + ns, stream, num_cus));
+    mark(3);
+    enqueued = true;
+    return BSG_OK;
+  }
+
+  int finish(uint64_t* nchunks) {
+    if (!enqueued) return BSG_ESTATE;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      HCHECK(hipMemcpyAsync(h_ctr.p, ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+      HCHECK(hipStreamSynchronize(stream));
+      last = *h_ctr.as<Counters>();
+      if (!last.overflow) break;
+      retry_cap = last.ncand + 1024;  // exact size for this input, then run again
+      int rc = enqueue();
+      if (rc) return rc;
+    }
+    retry_cap = 0;
+    if (last.overflow) return BSG_ENOMEM;
+    if (last.error) {
+      std::fprintf(stderr, "bsgpu: device sanity check failed (code %llu)\n",
+                   (unsigned long long)last.error);
+      enqueued = false;
+      return BSG_EDEVICE;
+    }
+    enqueued = false;
+    if (profile) {
+      for (int i = 0; i < 3; ++i)
+        if (hipEventElapsedTime(&stage_ms[i], ev[i], ev[i + 1]) != hipSuccess) {
+          (void)hipGetLastError();
+          stage_ms[i] = -1.f;
+        }
+    }
+    if (nchunks) *nchunks = last.nchunks;
+    return BSG_OK;
+  }
+};
+
+struct bsg_ctx {
+  bsg_engine* eng = nullptr;
+  bsg_params params{};
+  Params p{};
+  size_t tile = 256ull << 20;
+  PinBuf staging;
+  DevBuf dtile;
+  size_t fill = 0;
+  uint64_t pos = 0;         // stream bytes already handed to the device
+  uint64_t open_start = 0;  // open chunk start (stream offset)
+  uint64_t consumed = 0;    // open chunk bytes folded into mid
+  uint32_t prefix_len = 0;  // open chunk bytes not yet hashed (the tail of hist)
+  uint32_t mid[8];
+  uint8_t hist[64];
+  std::deque<bsg_chunk> ready;
+  std::vector<bsg_chunk> tmp;
+  bool closed = false;
+  int sticky = BSG_OK;
+
+  int process(bool final_seg) {
+    if (fill == 0 && !final_seg) return BSG_OK;
+    HCHECK(dtile.ensure(fill));
+    if (fill) HCHECK(hipMemcpyAsync(dtile.p, staging.p, fill, hipMemcpyHostToDevice, eng->stream));
+    StreamDesc d{};
+    d.data_off = 0;
+    d.len = fill;
+    d.seg_base = pos;
+    d.open_start = open_start;
+    d.consumed = consumed;
+    d.finalize = final_seg ? 1u : 0u;
+    d.prefix_len = prefix_len;
+    std::memcpy(d.mid, mid, sizeof mid);
+    std::memcpy(d.hist, hist, 64);
+    eng->d_data = dtile.as<uint8_t>();
+    eng->descs.assign(1, d);
+    eng->nstreams = 1;
+    eng->p = p;
+    int rc = eng->enqueue();
+    if (rc) return rc;
+    uint64_t n = 0;
+    rc = eng->finish(&n);
+    if (rc) return rc;
+    tmp.resize(n);
+    if (n)
+      HCHECK(hipMemcpy(tmp.data(), eng->out.p, sizeof(bsg_chunk) * n, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) ready.push_back(tmp[i]);
+    if (!final_seg) {
+      CarryOut co;
+      HCHECK(hipMemcpy(&co, eng->carry.p, sizeof co, hipMemcpyDeviceToHost));
+      if (!co.valid) return BSG_EDEVICE;
+      open_start = co.open_start;
+      consumed = co.consumed;
+      prefix_len = co.prefix_len;
+      std::memcpy(mid, co.mid, sizeof mid);
+    }
+    // window history = last 64 bytes of the stream so far
+    const uint8_t* seg = staging.as<uint8_t>();
+    if (fill >= 64) {
+      std::memcpy(hist, seg + fill - 64, 64);
+    } else if (fill) {
+      std::memmove(hist, hist + fill, 64 - fill);
+      std::memcpy(hist + 64 - fill, seg, fill);
+    }
+    pos += fill;
+    fill = 0;
+    return BSG_OK;
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* bsg_errstr(int err) {
+  switch (err) {
+    case BSG_OK: return "ok";
+    case BSG_EINVAL: return "invalid argument";
+    case BSG_ENOMEM: return "out of memory";
+    case BSG_EDEVICE: return "HIP device error";
+    case BSG_ESTATE: return "invalid state (write after close?)";
+    case BSG_ENODEV: return "no such HIP device";
+    default: return "unknown error";
+  }
+}
+
+bsg_params bsg_params_default(void) {
+  bsg_params p;
+  p.split_bits = 16;  // split/split.go:89
+  p.min_size = 1024;  // split/split.go:88
+  p.fanout = 8;       // split/split.go:48
+  p.reserved = 0;
+  return p;
+}
+
+void bsg_default_table(uint32_t out[256]) { std::memcpy(out, kBuzhash32Seed1, 1024); }
+
+int bsg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+bsg_engine* bsg_engine_create(int device, const uint32_t* table, int* err) {
+  int dummy;
+  if (!err) err = &dummy;
+  int n = bsg_device_count();
+  if (device < 0 || device >= n) {
+    *err = BSG_ENODEV;
+    return nullptr;
+  }
+  bsg_engine* e = new (std::nothrow) bsg_engine();
+  if (!e) {
+    *err = BSG_ENOMEM;
+    return nullptr;
+  }
+  e->dev = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    *err = BSG_EDEVICE;
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    e->num_cus = prop.multiProcessorCount;
+  if (e->table.ensure(1024) != hipSuccess ||
+      hipMemcpy(e->table.p, table ? table : kBuzhash32Seed1, 1024, hipMemcpyHostToDevice) !=
+          hipSuccess) {
+    bsg_engine_destroy(e);
+    *err = BSG_EDEVICE;
+    return nullptr;
+  }
+  *err = BSG_OK;
+  return e;
+}
+
+void bsg_engine_destroy(bsg_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->dev);
+  if (e->stream) hipStreamSynchronize(e->stream);
+  DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->slots,
+                    &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
+                    &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
+                    &e->out, &e->carry, &e->ctr};
+  for (DevBuf* b : bufs) b->release();
+  for (int i = 0; i < 4; ++i)
+    if (e->ev[i]) hipEventDestroy(e->ev[i]);
+  e->h_streams.release();
+  e->h_strip0.release();
+  e->h_ctr.release();
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int bsg_engine_run(bsg_engine* e, const uint8_t* d_data, const uint64_t* off, const uint64_t* len,
+                   uint32_t nstreams, const bsg_params* params) {
+  if (!e || (nstreams && (!d_data || !off || !len)) || nstreams > 65535) return BSG_EINVAL;
+  Params p;
+  int rc = normalize(params, &p, nullptr);
+  if (rc) return rc;
+  if ((rc = e->setdev())) return rc;
+  e->descs.assign(nstreams, StreamDesc{});
+  for (uint32_t s = 0; s < nstreams; ++s) {
+    if (off[s] % 16 != 0 || len[s] >= (1ull << 40)) return BSG_EINVAL;
+    StreamDesc& d = e->descs[s];
+    d.data_off = off[s];
+    d.len = len[s];
+    d.seg_base = 0;
+    d.open_start = 0;
+    d.consumed = 0;
+    d.finalize = 1;
+    d.prefix_len = 0;
+    std::memcpy(d.mid, kIV, sizeof kIV);
+  }
+  e->d_data = d_data;
+  e->nstreams = nstreams;
+  e->p = p;
+  return e->enqueue();
+}
+
+int bsg_engine_finish(bsg_engine* e, uint64_t* nchunks) {
+  if (!e) return BSG_EINVAL;
+  int rc = e->setdev();
+  if (rc) return rc;
+  return e->finish(nchunks);
+}
+
+const bsg_chunk* bsg_engine_chunks_device(const bsg_engine* e) {
+  return e ? static_cast<const bsg_chunk*>(e->out.p) : nullptr;
+}
+
+int bsg_engine_copy_chunks(bsg_engine* e, bsg_chunk* out, uint64_t cap) {
+  if (!e || (!out && cap)) return BSG_EINVAL;
+  int rc = e->setdev();
+  if (rc) return rc;
+  const uint64_t n = std::min<uint64_t>(cap, e->last.nchunks);
+  if (n) HCHECK(hipMemcpy(out, e->out.p, sizeof(bsg_chunk) * n, hipMemcpyDeviceToHost));
+  return BSG_OK;
+}
+
+int bsg_engine_copy_counts(bsg_engine* e, uint64_t* counts, uint32_t nstreams) {
+  if (!e || !counts || nstreams > e->nstreams) return BSG_EINVAL;
+  int rc = e->setdev();
+  if (rc) return rc;
+  if (nstreams)
+    HCHECK(hipMemcpy(counts, e->scount.p, sizeof(uint64_t) * nstreams, hipMemcpyDeviceToHost));
+  return BSG_OK;
+}
+
+void* bsg_engine_stream(bsg_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int bsg_engine_profile(bsg_engine* e, int enable) {
+  if (!e) return BSG_EINVAL;
+  int rc = e->setdev();
+  if (rc) return rc;
+  if (enable && !e->ev[0])
+    for (int i = 0; i < 4; ++i) HCHECK(hipEventCreate(&e->ev[i]));
+  e->profile = enable != 0;
+  return BSG_OK;
+}
+
+int bsg_engine_stage_ms(const bsg_engine* e, float out[3]) {
+  if (!e || !out || !e->profile) return BSG_EINVAL;
+  for (int i = 0; i < 3; ++i) out[i] = e->stage_ms[i];
+  return BSG_OK;
+}
+
+uint64_t bsg_engine_candidates(const bsg_engine* e) { return e ? e->last.ncand : 0; }
+
+bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, int* err) {
+  int dummy;
+  if (!err) err = &dummy;
+  Params p;
+  bsg_params norm;
+  int rc = normalize(params, &p, &norm);
+  if (rc) {
+    *err = rc;
+    return nullptr;
+  }
+  bsg_engine* e = bsg_engine_create(device, table, err);
+  if (!e) return nullptr;
+  bsg_ctx* c = new (std::nothrow) bsg_ctx();
+  if (!c) {
+    bsg_engine_destroy(e);
+    *err = BSG_ENOMEM;
+    return nullptr;
+  }
+  c->eng = e;
+  c->params = norm;
+  c->p = p;
+  std::memcpy(c->mid, kIV, sizeof kIV);
+  std::memset(c->hist, 0, 64);
+  *err = BSG_OK;
+  return c;
+}
+
+int bsg_set_tile(bsg_ctx* c, size_t tile) {
+  if (!c || tile < 4096 || c->fill || c->pos) return BSG_EINVAL;
+  c->tile = tile;
+  return BSG_OK;
+}
+
+int bsg_write(bsg_ctx* c, const uint8_t* p, size_t n) {
+  if (!c) return BSG_EINVAL;
+  if (c->closed) return BSG_ESTATE;
+  if (c->sticky) return c->sticky;
+  if (n && !p) return BSG_EINVAL;
+  int rc = c->eng->setdev();
+  if (rc) return rc;
+  if (n) HCHECK(c->staging.ensure(c->tile));
+  while (n) {
+    if (c->fill == c->tile) {  // full tile and more data coming: process it (never the last)
+      rc = c->process(false);
+      if (rc) return c->sticky = rc;
+    }
+    const size_t k = std::min(n, c->tile - c->fill);
+    std::memcpy(c->staging.as<uint8_t>() + c->fill, p, k);
+    c->fill += k;
+    p += k;
+    n -= k;
+  }
+  return BSG_OK;
+}
+
+int bsg_close(bsg_ctx* c) {
+  if (!c) return BSG_EINVAL;
+  if (c->closed) return c->sticky;
+  c->closed = true;
+  if (c->sticky) return c->sticky;
+  int rc = c->eng->setdev();
+  if (rc) return c->sticky = rc;
+  if (c->fill == 0 && c->pos == 0) return BSG_OK;  // empty stream: no chunks
+  rc = c->process(true);
+  if (rc) c->sticky = rc;
+  return rc;
+}
+
+size_t bsg_pending(const bsg_ctx* c) { return c ? c->ready.size() : 0; }
+
+size_t bsg_drain(bsg_ctx* c, bsg_chunk* out, size_t cap) {
+  if (!c || !out) return 0;
+  size_t k = 0;
+  while (k < cap && !c->ready.empty()) {
+    out[k++] = c->ready.front();
+    c->ready.pop_front();
+  }
+  return k;
+}
+
+void bsg_free(bsg_ctx* c) {
+  if (!c) return;
+  if (c->eng) {
+    hipSetDevice(c->eng->dev);
+    hipStreamSynchronize(c->eng->stream);
+  }
+  c->staging.release();
+  c->dtile.release();
+  bsg_engine_destroy(c->eng);
+  delete c;
+}
+
+int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* off,
+                         const uint64_t* len, uint32_t nstreams, const bsg_params* params,
+                         const uint32_t* table, bsg_chunk* out, uint64_t cap, uint64_t* counts,
+                         uint64_t* nchunks) {
+  if (nstreams && (!host_data || !off || !len)) return BSG_EINVAL;
+  int rc;
+  bsg_engine* e = bsg_engine_create(device, table, &rc);
+  if (!e) return rc;
+  // pack streams 16-byte aligned into one device buffer
+  std::vector<uint64_t> doff(nstreams);
+  uint64_t total = 0;
+  for (uint32_t s = 0; s < nstreams; ++s) {
+    doff[s] = total;
+    total += (len[s] + 15) & ~15ull;
+  }
+  DevBuf d;
+  if (d.ensure(total) != hipSuccess) {
+    bsg_engine_destroy(e);
+    return BSG_ENOMEM;
+  }
+  for (uint32_t s = 0; s < nstreams && rc == BSG_OK; ++s)
+    if (len[s] &&
+        hipMemcpy(static_cast<uint8_t*>(d.p) + doff[s], host_data + off[s], len[s],
+                  hipMemcpyHostToDevice) != hipSuccess)
+      rc = BSG_EDEVICE;
+  uint64_t n = 0;
+  if (rc == BSG_OK) rc = bsg_engine_run(e, d.as<uint8_t>(), doff.data(), len, nstreams, params);
+  if (rc == BSG_OK) rc = bsg_engine_finish(e, &n);
+  if (rc == BSG_OK && out) rc = bsg_engine_copy_chunks(e, out, cap);
+  if (rc == BSG_OK && counts) rc = bsg_engine_copy_counts(e, counts, nstreams);
+  if (nchunks) *nchunks = n;
+  d.release();
+  bsg_engine_destroy(e);
+  return rc;
+}
+
+int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed, void* stream) {
+  if (!d_ptr && nbytes) return BSG_EINVAL;
+  if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
+  HCHECK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  int cus = 256;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+  if (nbytes) HCHECK(launch_fill_splitmix(d_ptr, nbytes, seed, (hipStream_t)stream, cus));
+  return BSG_OK;
+}
+
+int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                     uint32_t n, uint8_t* refs) {
+  if (n && (!base || !off || !len || !refs)) return BSG_EINVAL;
+  if (n == 0) return BSG_OK;
+  if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
+  HCHECK(hipSetDevice(device));
+  hipPointerAttribute_t attr;
+  bool on_device = false;
+  if (hipPointerGetAttributes(&attr, base) == hipSuccess)
+    on_device = (attr.type == hipMemoryTypeDevice);
+  else
+    (void)hipGetLastError();
+  uint64_t hi = 0;
+  for (uint32_t i = 0; i < n; ++i) hi = std::max<uint64_t>(hi, off[i] + len[i]);
+  DevBuf dd, doff, dlen, drefs;
+  int rc = BSG_OK;
+  const uint8_t* dbase = base;
+  if (!on_device) {
+    if (dd.ensure(hi) != hipSuccess) return BSG_ENOMEM;
+    if (hi && hipMemcpy(dd.p, base, hi, hipMemcpyHostToDevice) != hipSuccess) rc = BSG_EDEVICE;
+    dbase = dd.as<uint8_t>();
+  }
+  if (rc == BSG_OK && (doff.ensure(8ull * n) != hipSuccess || dlen.ensure(8ull * n) != hipSuccess ||
+                       drefs.ensure(32ull * n) != hipSuccess))
+    rc = BSG_ENOMEM;
+  if (rc == BSG_OK && (hipMemcpy(doff.p, off, 8ull * n, hipMemcpyHostToDevice) != hipSuccess ||
+                       hipMemcpy(dlen.p, len, 8ull * n, hipMemcpyHostToDevice) != hipSuccess))
+    rc = BSG_EDEVICE;
+  if (rc == BSG_OK) {
+    hipDeviceProp_t prop;
+    int cus = 256;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+    BlobShaArgs a{dbase, doff.as<uint64_t>(), dlen.as<uint64_t>(), n, drefs.as<uint8_t>()};
+    if (launch_sha_blobs(a, nullptr, cus) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(refs, drefs.p, 32ull * n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = BSG_EDEVICE;
+  }
+  dd.release();
+  doff.release();
+  dlen.release();
+  drefs.release();
+  return rc;
+}
+
+}  // extern "C"

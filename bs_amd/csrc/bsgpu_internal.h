@@ -1,0 +1,90 @@
+// bsgpu_internal.h — device data layout shared by the HIP kernels and the host engine.
+//
+// One launch ("run") processes a batch of stream SEGMENTS. A segment is a contiguous range of
+// one byte stream that lives in device memory. Fresh streams (the batch API) have zero history,
+// IV hash state and finalize=1. Streaming continuation (split.Writer over many Write calls,
+// reference split/split.go:99-126) carries a 64-byte window history, the open chunk's start
+// and its SHA-256 midstate from one segment to the next.
+#pragma once
+#include <stdint.h>
+
+namespace bsg {
+
+constexpr int kScanWG = 512;       // threads per rolling-scan workgroup (8 waves)
+constexpr int kStrip = 2048;       // bytes per lane-strip in the rolling scan
+constexpr int kSlotCap = 4;        // candidates kept per strip in the first scan pass
+constexpr int kTabRows = 256;      // buzhash32 table rows
+constexpr int kTabRep = 64;        // one replica per lane: LDS address = byte*256 + lane*4
+
+// Candidate record (u64): | stream:16 | pos:40 | force:1 | unused:1 | tz:6 |
+constexpr int kCandPosShift = 8;
+constexpr uint64_t kCandPosMask = (1ull << 40) - 1;
+constexpr uint64_t kCandForce = 1ull << 7;
+
+__host__ __device__ inline uint64_t cand_pack(uint32_t stream, uint64_t pos, bool force,
+                                              uint32_t tz) {
+  return ((uint64_t)stream << 48) | ((pos & kCandPosMask) << kCandPosShift) |
+         (force ? kCandForce : 0ull) | (uint64_t)(tz & 63u);
+}
+__host__ __device__ inline uint32_t cand_stream(uint64_t c) { return (uint32_t)(c >> 48); }
+__host__ __device__ inline uint64_t cand_pos(uint64_t c) {
+  return (c >> kCandPosShift) & kCandPosMask;
+}
+__host__ __device__ inline bool cand_force(uint64_t c) { return (c & kCandForce) != 0; }
+__host__ __device__ inline uint32_t cand_tz(uint64_t c) { return (uint32_t)(c & 63u); }
+
+// Per-strip slot record (u32): | local_off:24 | force:1 | unused:1 | tz:6 |
+__host__ __device__ inline uint32_t slot_pack(uint32_t local, bool force, uint32_t tz) {
+  return (local << 8) | (force ? 0x80u : 0u) | (tz & 63u);
+}
+
+struct StreamDesc {            // 160 bytes, 16-byte aligned
+  uint64_t data_off;           // device byte offset of the segment's first byte
+  uint64_t len;                // segment length (bytes)
+  uint64_t strip0;             // first global strip index of this segment
+  uint64_t seg_base;           // stream offset of the segment's first byte
+  uint64_t open_start;         // stream offset where the open (unfinished) chunk starts
+  uint64_t consumed;           // open-chunk bytes already folded into mid[] (multiple of 64)
+  uint32_t finalize;           // 1: flush the tail as the final chunk (Splitter.Close)
+  uint32_t prefix_len;         // open-chunk bytes held in hist[64-prefix_len..63], < 64
+  uint32_t mid[8];             // SHA-256 midstate of the open chunk (IV when consumed == 0)
+  uint32_t pad_[2];
+  uint8_t hist[64];            // the 64 stream bytes before seg_base (zeros before offset 0)
+};
+static_assert(sizeof(StreamDesc) == 160, "StreamDesc layout");
+
+struct CarryOut {              // open chunk state after a non-final segment
+  uint32_t mid[8];
+  uint64_t consumed;           // bytes folded into mid (multiple of 64)
+  uint64_t open_start;         // stream offset of the open chunk
+  uint32_t prefix_len;         // trailing open-chunk bytes not yet hashed (< 64)
+  uint32_t valid;
+};
+
+struct ChunkRec {              // == bsg_chunk (include/bsgpu.h)
+  uint64_t offset;
+  uint64_t len;
+  uint32_t level;
+  uint32_t stream;
+  uint8_t ref[32];
+};
+static_assert(sizeof(ChunkRec) == 56, "ChunkRec layout");
+
+struct Params {
+  uint32_t split_bits;         // trailing-zero bits for a boundary (1..32)
+  uint32_t min_size;           // minimum chunk size (>= 64)
+  uint32_t mask;               // (1 << split_bits) - 1
+  uint32_t pad_;
+};
+
+// Device counters, zeroed at the start of every run (one hipMemsetAsync).
+struct Counters {
+  uint64_t ncand;              // total candidates (from the strip-count scan)
+  uint64_t nchunks;            // total boundaries = finalized chunks
+  uint64_t job_head;           // SHA-256 dynamic work queue head
+  uint64_t overflow;           // candidate buffer too small (host grows and re-runs)
+  uint64_t error;              // device-side sanity check failed (bug guard; run is invalid)
+  uint64_t pad_[3];
+};
+
+}  // namespace bsg

@@ -1,0 +1,740 @@
+// bsgpu_kernels.hip — CDNA4 (gfx950) kernels for BS's hashsplit chunker + SHA-256 refs.
+//
+// Pipeline for one run over a batch of stream segments (see bsgpu_internal.h):
+//   k_scan      rolling buzhash32 over every byte position, one lane per 2 KiB strip,
+//               64-byte window history kept in VGPRs, 64-way replicated table in LDS
+//               (conflict-free ds_read_b32), candidates (tz >= split_bits) into per-strip slots
+//   scan_*      exclusive prefix sums (strip counts -> candidate offsets; flags -> chunk index)
+//   k_compact   slots -> one sorted candidate list (re-scans the rare overflowing strips)
+//   k_select    MinSize greedy as independent walks between "sync points"
+//   k_chunks    boundary list + per-stream counts
+//   k_sha       batched variable-length SHA-256, one lane per chunk, dynamic per-lane queue
+//
+// Reference semantics being reproduced: hashsplit.Splitter as wired by split.NewWriter
+// (/root/reference/split/split.go:85-89) and bs.Blob.Ref = sha256 (/root/reference/bs.go:24-26).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "bsgpu_internal.h"
+#include "bsgpu_launch.h"
+
+namespace bsg {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(16)));
+
+__device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t r) {
+  return __builtin_amdgcn_alignbit(x, x, r);
+}
+// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t tz32(uint32_t h) { return h ? (uint32_t)__builtin_ctz(h) : 32u; }
+
+__device__ __forceinline__ void load16(const uint8_t* p, uint32_t (&w)[16]) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u32x4 v = q[i];
+    w[4 * i + 0] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+
+// LDS byte address of table row `byte k of word w` in this lane's replica: byte*256 + lane*4,
+// built by one v_perm_b32: D.b0 = lane4, D.b1 = w.b[k], D.b2 = D.b3 = 0.
+__device__ __forceinline__ uint32_t tab_addr(uint32_t w, uint32_t lane4, int k) {
+  // k is a compile-time constant after unrolling, so the selector is an inline literal
+  return __builtin_amdgcn_perm(w, lane4, 0x0c0c0400u | ((4u + (uint32_t)(k & 3)) << 8));
+}
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* tab, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(tab) + byte_addr);
+}
+__device__ __forceinline__ uint32_t lookup(const uint32_t* tab, uint32_t w, uint32_t lane4,
+                                           int k) {
+  return lds_u32(tab, tab_addr(w, lane4, k));
+}
+
+__device__ __forceinline__ void load_table(uint32_t* tab, const uint32_t* __restrict__ T) {
+  // 256 rows x 64 replicas; each uint4 store writes 4 replicas of one row.
+  u32x4a* t4 = reinterpret_cast<u32x4a*>(tab);
+  for (uint32_t i = threadIdx.x; i < kTabRows * kTabRep / 4; i += blockDim.x) {
+    uint32_t v = T[i >> 4];
+    t4[i] = u32x4a{v, v, v, v};
+  }
+}
+
+__device__ __forceinline__ uint32_t find_stream(const uint64_t* __restrict__ strip0, uint32_t n,
+                                                uint64_t strip) {
+  // largest s in [0, n) with strip0[s] <= strip (zero-length streams are skipped)
+  uint32_t lo = 0, hi = n;  // invariant: strip0[lo] <= strip < strip0[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (strip0[mid] <= strip) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Rolling scan of one strip.
+// h(p) = XOR_{k<64} rotl(T[x[p-k]], k mod 32): after warming the window with the 64 bytes
+// before the strip (stream history / zeros), each byte costs one LDS lookup, one rotate and
+// one 3-way xor; the outgoing byte's table value comes from the 64-entry VGPR history.
+// ---------------------------------------------------------------------------------------------
+struct StripCtx {
+  uint32_t stream;
+  uint64_t start;      // segment offset of the strip
+  uint32_t count;      // candidates found so far
+  uint64_t wbase;      // WRITE mode: first output index
+  uint64_t seg_base;
+};
+
+template <bool WRITE>
+__device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t strip,
+                                     uint64_t seg_off, bool force, uint32_t tz) {
+  if (WRITE) {
+    uint64_t idx = c.wbase + c.count;
+    if (idx < a.cand_cap) a.cand[idx] = cand_pack(c.stream, c.seg_base + seg_off, force, tz);
+  } else {
+    if (c.count < (uint32_t)kSlotCap)
+      a.slots[strip * kSlotCap + c.count] = slot_pack((uint32_t)(seg_off - c.start), force, tz);
+  }
+  c.count++;
+}
+
+template <bool WRITE>
+__device__ __forceinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
+                                        const uint8_t* d, const StreamDesc* sd, StripCtx& c,
+                                        uint64_t strip, uint64_t off, uint32_t h,
+                                        const uint32_t (&w)[16]) {
+  uint32_t pw[16];
+  if (off >= 64) load16(d + off - 64, pw);
+  else load16(sd->hist, pw);
+  const uint32_t mask = a.p.mask;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
+    uint32_t tout = lookup(tab, pw[k >> 2], lane4, k);
+    h = xor3(rotl1(h), tout, tin);
+    if ((h & mask) == 0) emit<WRITE>(a, c, strip, off + k, false, tz32(h));
+  }
+}
+
+template <bool WRITE>
+__device__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
+                               uint64_t strip, uint64_t wbase) {
+  StripCtx c;
+  c.stream = find_stream(a.strip0, a.nstreams, strip);
+  const StreamDesc* sd = a.streams + c.stream;
+  const uint64_t seglen = sd->len;
+  c.start = (strip - sd->strip0) * (uint64_t)kStrip;
+  c.count = 0;
+  c.wbase = wbase;
+  c.seg_base = sd->seg_base;
+  const uint32_t len = (uint32_t)min((uint64_t)kStrip, seglen - c.start);
+  const uint8_t* d = a.data + sd->data_off;
+  const uint32_t mask = a.p.mask;
+
+  uint32_t w[16];
+  if (c.start >= 64) load16(d + c.start - 64, w);
+  else load16(sd->hist, w);
+  uint32_t hist[64];
+  uint32_t h = 0;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    uint32_t t = lookup(tab, w[k >> 2], lane4, k);
+    h = rotl1(h) ^ t;
+    hist[k] = t;
+  }
+
+  const uint32_t nfull = len >> 6;
+  if (nfull) load16(d + c.start, w);
+  for (uint32_t b = 0; b < nfull; ++b) {
+    const uint64_t off = c.start + 64ull * b;
+    uint32_t wn[16];
+    load16(d + c.start + 64ull * min(b + 1, nfull - 1), wn);  // prefetch (clamped, branchless)
+    const uint32_t h0 = h;
+    uint32_t m = 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      uint32_t t = lookup(tab, w[k >> 2], lane4, k);
+      h = xor3(rotl1(h), hist[k], t);
+      hist[k] = t;
+      m = min(m, h & mask);
+    }
+    if (__builtin_expect(m == 0, 0)) slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, off, h0, w);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = wn[i];
+  }
+
+  const uint32_t rem = len & 63u;
+  if (rem) {  // tail of the segment: byte loads, never past the end
+    const uint64_t off = c.start + 64ull * nfull;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      if ((uint32_t)k < rem) {
+        uint32_t byte = d[off + k];
+        uint32_t t = lds_u32(tab, (byte << 8) | lane4);
+        h = xor3(rotl1(h), hist[k], t);
+        hist[k] = t;
+        if ((h & mask) == 0) emit<WRITE>(a, c, strip, off + k, false, tz32(h));
+      }
+    }
+  }
+  if (c.start + len == seglen && sd->finalize) {
+    // Splitter.Close(): the remainder becomes the final chunk; level from the same check.
+    emit<WRITE>(a, c, strip, seglen - 1, true, tz32(h));
+  }
+  return c.count;
+}
+
+__global__ __launch_bounds__(kScanWG, 4) void k_scan(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+  load_table(tab, a.table);
+  __syncthreads();
+  const uint32_t lane4 = (threadIdx.x & 63u) << 2;
+  for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
+    const uint64_t strip = g * kScanWG + threadIdx.x;
+    if (strip < a.nstrips) a.counts[strip] = scan_strip<false>(a, tab, lane4, strip, 0);
+  }
+}
+
+__global__ __launch_bounds__(kScanWG, 4) void k_compact(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+  if (a.ctr->overflow) return;
+  bool loaded = false;
+  const uint32_t lane4 = (threadIdx.x & 63u) << 2;
+  for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
+    const uint64_t strip = g * kScanWG + threadIdx.x;
+    const uint32_t cnt = strip < a.nstrips ? a.counts[strip] : 0u;
+    const bool need = cnt > (uint32_t)kSlotCap;
+    if (__syncthreads_or(need) && !loaded) {
+      load_table(tab, a.table);
+      __syncthreads();
+      loaded = true;
+    }
+    if (cnt == 0) continue;
+    const uint64_t base = a.cand_off[strip];
+    if (!need) {
+      const uint32_t s = find_stream(a.strip0, a.nstreams, strip);
+      const StreamDesc* sd = a.streams + s;
+      const uint64_t start = sd->seg_base + (strip - sd->strip0) * (uint64_t)kStrip;
+      for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t v = a.slots[strip * kSlotCap + i];
+        if (base + i < a.cand_cap)
+          a.cand[base + i] = cand_pack(s, start + (v >> 8), (v & 0x80u) != 0, v & 63u);
+      }
+    } else {
+      scan_strip<true>(a, tab, lane4, strip, base);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Exclusive prefix sum u32 -> u64 (three phases). n is min(n_bound, *n_dev) when n_dev != null.
+// ---------------------------------------------------------------------------------------------
+constexpr int kScanT = 256, kScanItems = 8, kScanTile = kScanT * kScanItems;
+
+__device__ __forceinline__ uint64_t scan_n(const PrefixArgs& a) {
+  uint64_t n = a.n_bound;
+  if (a.n_dev) n = min(n, *a.n_dev);
+  return n;
+}
+
+__global__ __launch_bounds__(kScanT) void k_prefix_reduce(PrefixArgs a) {
+  __shared__ uint64_t red[kScanT / 64];
+  if (a.skip_if && *a.skip_if) return;
+  const uint64_t n = scan_n(a);
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  if (base >= n) {
+    if (threadIdx.x == 0) a.partials[blockIdx.x] = 0;
+    return;
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    const uint64_t idx = base + (uint64_t)i * kScanT + threadIdx.x;
+    if (idx < n) s += a.in[idx];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) a.partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(1024) void k_prefix_top(PrefixArgs a, uint64_t nblocks) {
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t carry;
+  if (a.skip_if && *a.skip_if) return;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < nblocks; base += 1024) {
+    const uint64_t i = base + threadIdx.x;
+    const uint64_t v = i < nblocks ? a.partials[i] : 0;
+    uint64_t x = v;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o);
+      if ((threadIdx.x & 63) >= (uint32_t)o) x += y;
+    }
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (uint32_t wv = 0; wv < (threadIdx.x >> 6); ++wv) pre += wsum[wv];
+    if (i < nblocks) a.partials[i] = pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = pre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *a.total = carry;
+    if (a.overflow && carry > a.cap) *a.overflow = 1;
+  }
+}
+
+__global__ __launch_bounds__(kScanT) void k_prefix_down(PrefixArgs a) {
+  __shared__ uint64_t wsum[kScanT / 64];
+  if (a.skip_if && *a.skip_if) return;
+  const uint64_t n = scan_n(a);
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  if (base >= n) return;
+  // thread t owns kScanItems consecutive elements
+  const uint64_t first = base + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = (first + i < n) ? a.in[first + i] : 0u;
+    s += v[i];
+  }
+  uint64_t x = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o);
+    if ((threadIdx.x & 63) >= (uint32_t)o) x += y;
+  }
+  if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint64_t pre = a.partials[blockIdx.x];
+  for (uint32_t wv = 0; wv < (threadIdx.x >> 6); ++wv) pre += wsum[wv];
+  pre += x - s;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (first + i < n) a.out[first + i] = pre;
+    pre += v[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MinSize greedy selection. A candidate whose distance to its predecessor (or to the open
+// chunk's start) is >= MinSize is a boundary whatever came before ("sync point"), so the
+// greedy chain restarts there: one lane walks each run of candidates between sync points.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_select(SelArgs a) {
+  if (a.ctr->overflow) return;
+  const uint64_t total = a.ctr->ncand;
+  const uint64_t minsz = a.p.min_size;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const uint64_t c = a.cand[i];
+    const uint32_t s = cand_stream(c);
+    const uint64_t E = cand_pos(c) + 1;  // end (exclusive) if this candidate is a boundary
+    const bool first = (i == 0) || cand_stream(a.cand[i - 1]) != s;
+    uint64_t last, j;
+    if (first) {
+      last = a.streams[s].open_start;
+      j = i;
+    } else {
+      const uint64_t pE = cand_pos(a.cand[i - 1]) + 1;
+      if (E - pE < minsz) continue;  // not a sync point: covered by an earlier walk
+      a.flags[i] = 1;
+      last = E;
+      j = i + 1;
+    }
+    uint64_t prevE = first ? 0 : E;
+    for (; j < total; ++j) {
+      const uint64_t cj = a.cand[j];
+      if (cand_stream(cj) != s) break;
+      const uint64_t Ej = cand_pos(cj) + 1;
+      if (j > i && Ej - prevE >= minsz) break;  // next sync point starts its own walk
+      const bool f = cand_force(cj) ? (Ej > last) : (Ej - last >= minsz);
+      a.flags[j] = f ? 1u : 0u;
+      if (f) last = Ej;
+      prevE = Ej;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_chunks(ChunkArgs a) {
+  if (a.ctr->overflow) return;
+  const uint64_t total = a.ctr->ncand;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t bits = a.p.split_bits;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    if (!a.flags[i]) continue;
+    const uint64_t c = a.cand[i];
+    const uint64_t k = a.fidx[i];
+    const uint32_t s = cand_stream(c);
+    const uint32_t tz = cand_tz(c);
+    const uint32_t level = tz >= bits ? tz - bits : 0u;
+    const uint64_t E = cand_pos(c) + 1;
+    if (k >= a.chunk_cap) {  // cannot happen if selection is right (chunks >= MinSize)
+      atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 1ull);
+      continue;
+    }
+    a.bnd_end[k] = E;
+    a.bnd_info[k] = ((uint64_t)s << 32) | level;
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.scount + s), 1ull);
+    atomicMax(reinterpret_cast<unsigned long long*>(a.last_end + s), (unsigned long long)E);
+  }
+}
+
+__global__ void k_init(InitArgs a) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < a.nstreams;
+       s += gridDim.x * blockDim.x) {
+    a.last_end[s] = a.streams[s].open_start;
+    a.scount[s] = 0;
+    a.carry[s].valid = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Batched variable-length SHA-256 (FIPS 180-4). One lane = one chunk at a time; lanes pull
+// jobs from a device queue as they finish, so a wave stays full whatever the length mix.
+// Jobs [0, M) are finished chunks; jobs [M, M + nstreams) are the open chunks of non-final
+// segments (hash whole blocks only, export the midstate).
+// ---------------------------------------------------------------------------------------------
+__constant__ uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+    0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+    0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+    0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+    0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+    0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+    0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+    0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2};
+
+__device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&W)[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    if (t >= 16) {
+      const uint32_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+      W[t & 15] += s0 + W[(t - 7) & 15] + s1;
+    }
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = (e & f) | (~e & g);
+    const uint32_t t1 = h + S1 + ch + kK256[t] + W[t & 15];
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t ab = a ^ b;
+    const uint32_t mj = (ab & c) | (~ab & b);
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + mj;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+struct ShaJob {
+  uint64_t id;          // job index
+  uint64_t start, end;  // stream offsets [start, end)
+  const uint8_t* dbase; // first data byte of this launch's part of the message
+  const uint8_t* hist;  // prefix bytes (the open chunk's unhashed head), prefix_len of them
+  uint64_t L;           // message bytes available this launch (prefix + data)
+  uint64_t consumed;    // bytes already folded into the init state
+  uint32_t prefix;
+  uint32_t nblocks;
+  uint32_t fin;
+  uint32_t level;
+  uint32_t stream;
+};
+
+__device__ bool sha_setup(const ShaArgs& a, uint64_t j, uint64_t M, ShaJob& jb,
+                          uint32_t (&st)[8]) {
+  uint32_t s;
+  if (j < M) {
+    const uint64_t info = a.bnd_info[j];
+    s = (uint32_t)(info >> 32);
+    jb.level = (uint32_t)info;
+    jb.end = a.bnd_end[j];
+    const StreamDesc* sd = a.streams + s;
+    jb.start = (j > 0 && (uint32_t)(a.bnd_info[j - 1] >> 32) == s) ? a.bnd_end[j - 1]
+                                                                  : sd->open_start;
+    jb.fin = 1;
+  } else {
+    s = (uint32_t)(j - M);
+    const StreamDesc* sd = a.streams + s;
+    if (sd->finalize) return false;
+    jb.start = a.last_end[s];
+    jb.end = sd->seg_base + sd->len;
+    jb.level = 0;
+    jb.fin = 0;
+  }
+  const StreamDesc* sd = a.streams + s;
+  jb.id = j;
+  jb.stream = s;
+  uint64_t dstart;
+  if (jb.start < sd->seg_base) {  // continues the open chunk of the previous segment
+    jb.prefix = sd->prefix_len;
+    jb.consumed = sd->consumed;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = sd->mid[i];
+    dstart = 0;
+  } else {
+    jb.prefix = 0;
+    jb.consumed = 0;
+    st[0] = 0x6a09e667; st[1] = 0xbb67ae85; st[2] = 0x3c6ef372; st[3] = 0xa54ff53a;
+    st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
+    dstart = jb.start - sd->seg_base;
+  }
+  jb.dbase = a.data + sd->data_off + dstart;
+  jb.hist = sd->hist + 64 - jb.prefix;
+  if (jb.end < jb.start || jb.end > sd->seg_base + sd->len || jb.start < sd->open_start) {
+    atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);  // bug guard
+    return false;
+  }
+  jb.L = jb.prefix + (jb.end - sd->seg_base - dstart);
+  jb.nblocks = jb.fin ? (uint32_t)((jb.L + 8) / 64 + 1) : (uint32_t)(jb.L / 64);
+  return true;
+}
+
+__device__ __forceinline__ void sha_load_fast(const uint8_t* p, uint32_t (&W)[16]) {
+  // 16 big-endian words from an arbitrary byte address: aligned dword loads + v_perm_b32
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+  const uint32_t sh = (uint32_t)(addr & 3u);
+  const uint32_t* al = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  uint32_t r[17];
+  const u32x4* q = reinterpret_cast<const u32x4*>(al);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u32x4 v = q[i];
+    r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+  }
+  r[16] = sh ? al[16] : 0u;  // an aligned dword holding a needed byte never crosses a page
+  const uint32_t sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(r[i + 1], r[i], sel);
+}
+
+__device__ __forceinline__ void sha_load_slow(const ShaJob& jb, uint32_t blk, uint32_t (&W)[16]) {
+  const uint64_t o0 = 64ull * blk;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint64_t o = o0 + 4 * q + r;
+      uint32_t byte;
+      if (o < jb.prefix) byte = jb.hist[o];
+      else if (o < jb.L) byte = jb.dbase[o - jb.prefix];
+      else byte = (o == jb.L) ? 0x80u : 0u;
+      word = (word << 8) | byte;
+    }
+    W[q] = word;
+  }
+  if (jb.fin && blk + 1 == jb.nblocks) {
+    const uint64_t bits = (jb.consumed + jb.L) * 8ull;
+    W[14] = (uint32_t)(bits >> 32);
+    W[15] = (uint32_t)bits;
+  }
+}
+
+__device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&st)[8]) {
+  if (jb.fin) {
+    ChunkRec* r = a.out + jb.id;
+    r->offset = jb.start;
+    r->len = jb.end - jb.start;
+    r->level = jb.level;
+    r->stream = jb.stream;
+    uint32_t* ref = reinterpret_cast<uint32_t*>(r->ref);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ref[i] = __builtin_bswap32(st[i]);
+  } else {
+    CarryOut* co = a.carry + jb.stream;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) co->mid[i] = st[i];
+    co->consumed = jb.consumed + 64ull * jb.nblocks;
+    co->open_start = jb.start;
+    co->prefix_len = (uint32_t)(jb.L & 63u);
+    co->valid = 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sha(ShaArgs a) {
+  if (a.ctr->overflow || a.ctr->error) return;
+  const uint64_t M = a.ctr->nchunks;
+  if (M > a.chunk_cap) return;  // k_chunks flagged the error
+  const uint64_t njobs = M + a.nstreams;
+  ShaJob jb;
+  uint32_t st[8];
+  bool has = false, exhausted = false;
+  uint32_t blk = 0;
+  for (;;) {
+    while (!has && !exhausted) {
+      const uint64_t j = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->job_head), 1ull);
+      if (j >= njobs) {
+        exhausted = true;
+      } else if (sha_setup(a, j, M, jb, st)) {
+        blk = 0;
+        if (jb.nblocks == 0) sha_finish(a, jb, st);
+        else has = true;
+      }
+    }
+    if (!has) break;
+    uint32_t W[16];
+    const uint64_t o0 = 64ull * blk;
+    if (o0 >= jb.prefix && o0 + 64 <= jb.L) sha_load_fast(jb.dbase + (o0 - jb.prefix), W);
+    else sha_load_slow(jb, blk, W);
+    sha256_compress(st, W);
+    if (++blk == jb.nblocks) {
+      sha_finish(a, jb, st);
+      has = false;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Standalone batched SHA-256 over (offset, length) blobs (bsg_sha256_batch).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sha_blobs(BlobShaArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    ShaJob jb;
+    jb.id = i;
+    jb.start = 0;
+    jb.end = a.len[i];
+    jb.dbase = a.base + a.off[i];
+    jb.hist = nullptr;
+    jb.L = a.len[i];
+    jb.consumed = 0;
+    jb.prefix = 0;
+    jb.fin = 1;
+    jb.nblocks = (uint32_t)((jb.L + 8) / 64 + 1);
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    for (uint32_t blk = 0; blk < jb.nblocks; ++blk) {
+      uint32_t W[16];
+      const uint64_t o0 = 64ull * blk;
+      if (o0 + 64 <= jb.L) sha_load_fast(jb.dbase + o0, W);
+      else sha_load_slow(jb, blk, W);
+      sha256_compress(st, W);
+    }
+    uint32_t* ref = reinterpret_cast<uint32_t*>(a.refs + 32 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ref[k] = __builtin_bswap32(st[k]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic input (bench/test utility, not on the hot path): word i = splitmix64(seed+(i+1)*G)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fill_splitmix(uint8_t* p, uint64_t n, uint64_t seed) {
+  const uint64_t nw = (n + 7) / 8;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (8 * i + 8 <= n) {
+      *reinterpret_cast<uint64_t*>(p + 8 * i) = z;
+    } else {
+      for (uint64_t b = 0; 8 * i + b < n; ++b) p[8 * i + b] = (uint8_t)(z >> (8 * b));
+    }
+  }
+}
+
+hipError_t launch_fill_splitmix(uint8_t* p, uint64_t n, uint64_t seed, hipStream_t s,
+                                int num_cus) {
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n / 8 + 255) / 256 + 1, 16ull * num_cus);
+  hipLaunchKernelGGL(k_fill_splitmix, dim3(grid), dim3(256), 0, s, p, n, seed);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------------
+static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap) {
+  uint64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (uint32_t)(g < cap ? g : cap);
+}
+
+hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
+  const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
+  const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_scan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus) {
+  const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
+  const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
+  return hipGetLastError();
+}
+
+uint64_t prefix_partials_needed(uint64_t n_bound) {
+  return (n_bound + kScanTile - 1) / kScanTile + 1;
+}
+
+hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s) {
+  const uint64_t nb = (a.n_bound + kScanTile - 1) / kScanTile;
+  if (nb == 0) {
+    hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(1024), 0, s, a, (uint64_t)0);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_prefix_reduce, dim3((uint32_t)nb), dim3(kScanT), 0, s, a);
+  hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(1024), 0, s, a, nb);
+  hipLaunchKernelGGL(k_prefix_down, dim3((uint32_t)nb), dim3(kScanT), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus) {
+  const uint32_t grid = grid_for(cand_bound, 256, 8u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_select, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus) {
+  const uint32_t grid = grid_for(cand_bound, 256, 8u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_chunks, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_init(const InitArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_init, dim3(grid_for(a.nstreams, 256, 1024)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
+  // enough lanes for every job, capped at ~8 waves per SIMD; idle lanes exit at once
+  const uint32_t grid = grid_for(job_bound, 256, 8u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_sha, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus) {
+  const uint32_t grid = grid_for(a.n, 256, 8u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_sha_blobs, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace bsg

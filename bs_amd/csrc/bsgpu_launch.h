@@ -1,0 +1,100 @@
+// bsgpu_launch.h — kernel argument blocks and launchers (host <-> bsgpu_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bsgpu_internal.h"
+
+namespace bsg {
+
+struct ScanArgs {
+  const uint8_t* data;
+  const StreamDesc* streams;
+  const uint64_t* strip0;   // nstreams + 1 cumulative strip counts
+  uint32_t nstreams;
+  uint64_t nstrips;
+  const uint32_t* table;    // 256 buzhash32 entries
+  Params p;
+  uint32_t* counts;         // [nstrips]
+  uint32_t* slots;          // [nstrips * kSlotCap]
+  const uint64_t* cand_off; // [nstrips] exclusive candidate offsets (compact)
+  uint64_t* cand;           // [cand_cap]
+  uint64_t cand_cap;
+  Counters* ctr;
+};
+
+struct PrefixArgs {
+  const uint32_t* in;
+  uint64_t* out;
+  uint64_t* partials;
+  uint64_t n_bound;         // host bound on n
+  const uint64_t* n_dev;    // optional device-side n (min with n_bound)
+  uint64_t* total;          // receives the sum
+  uint64_t* overflow;       // optional: set to 1 when total > cap
+  uint64_t cap;
+  const uint64_t* skip_if;  // optional: skip when *skip_if != 0
+};
+
+struct SelArgs {
+  const uint64_t* cand;
+  const StreamDesc* streams;
+  uint32_t* flags;
+  Params p;
+  Counters* ctr;
+};
+
+struct ChunkArgs {
+  const uint64_t* cand;
+  const uint32_t* flags;
+  const uint64_t* fidx;
+  uint64_t* bnd_end;
+  uint64_t* bnd_info;
+  uint64_t* scount;
+  uint64_t* last_end;
+  uint64_t chunk_cap;
+  Params p;
+  Counters* ctr;
+};
+
+struct InitArgs {
+  const StreamDesc* streams;
+  uint32_t nstreams;
+  uint64_t* last_end;
+  uint64_t* scount;
+  CarryOut* carry;
+};
+
+struct ShaArgs {
+  const uint8_t* data;
+  const StreamDesc* streams;
+  uint32_t nstreams;
+  const uint64_t* bnd_end;
+  const uint64_t* bnd_info;
+  const uint64_t* last_end;
+  Counters* ctr;
+  ChunkRec* out;
+  CarryOut* carry;
+  uint64_t chunk_cap;
+};
+
+struct BlobShaArgs {
+  const uint8_t* base;
+  const uint64_t* off;
+  const uint64_t* len;
+  uint64_t n;
+  uint8_t* refs;            // [n * 32]
+};
+
+hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus);
+hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus);
+uint64_t prefix_partials_needed(uint64_t n_bound);
+hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s);
+hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);
+hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);
+hipError_t launch_init(const InitArgs& a, hipStream_t s);
+hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
+hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus);
+hipError_t launch_fill_splitmix(uint8_t* p, uint64_t n, uint64_t seed, hipStream_t s,
+                                int num_cus);
+
+}  // namespace bsg

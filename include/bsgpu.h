@@ -1,0 +1,130 @@
+/*
+ * bsgpu.h — C ABI of libbsgpu, the MI355X (gfx950) ingest path for BS's hashsplit chunker and
+ * SHA-256 blob refs. Plain pointers and sizes only; no C++ exceptions cross this boundary.
+ *
+ * Reference interfaces replaced (paths relative to the bobg/bs tree):
+ *   bsg_open / bsg_write / bsg_close / bsg_drain
+ *       -> split.NewWriter(ctx, st, opts...)            split/split.go:44-96
+ *          (*split.Writer).Write([]byte) (int, error)   split/split.go:99-101
+ *          (*split.Writer).Close() error                split/split.go:104-126
+ *          options Bits / MinSize / Fanout               split/split.go:137,148,161
+ *       The per-byte loop they replace is hashsplit.Splitter.Write/Close (github.com/bobg/hashsplit
+ *       v1.1.1, go.mod:9) with buzhash32 (github.com/chmduquesne/rollinghash v4.0.0, go.sum:61-62).
+ *       The chunk records carry the ref that st.Put would compute (split/split.go:72 ->
+ *       store/mem/mem.go:67 -> bs.go:24-26); the caller still calls its own Store.Put.
+ *   bsg_sha256_batch
+ *       -> bs.Blob.Ref() = sha256.Sum256(b)              bs.go:24-26 (many blobs at once)
+ *   bsg_engine_* (device-resident batch of independent streams)
+ *       -> N concurrent split.Writers, e.g. fs.Dir.AddDir's per-file writers (fs/dir.go:157-174)
+ *
+ * Threading: one bsg_ctx / bsg_engine per thread at a time; different contexts are
+ * independent (each owns a HIP stream) and may run concurrently. Every entry point makes the
+ * context's device current (hipSetDevice) so callers may migrate between OS threads.
+ *
+ * Errors: functions return BSG_OK (0) or a negative code; bsg_errstr() describes it.
+ */
+#ifndef BSGPU_H
+#define BSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BSG_OK 0
+#define BSG_EINVAL (-22)   /* bad argument (e.g. min_size < 64, split_bits > 32) */
+#define BSG_ENOMEM (-12)   /* host or device allocation failed */
+#define BSG_EDEVICE (-5)   /* HIP runtime / kernel error */
+#define BSG_ESTATE (-71)   /* Write after Close, etc. */
+#define BSG_ENODEV (-19)   /* no such HIP device */
+
+/* split.Writer options. Zero fields take hashsplit's own defaults (SplitBits 13, MinSize 64);
+ * bsg_params_default() gives split.NewWriter's defaults (16 / 1024 / fanout 8,
+ * split/split.go:48,88-89). */
+typedef struct bsg_params {
+  uint32_t split_bits; /* Bits(n): trailing zero bits for a boundary, 1..32 */
+  uint32_t min_size;   /* MinSize(n): minimum chunk size, >= 64 */
+  uint32_t fanout;     /* Fanout(n): tree level divisor (host tree only), >= 1 */
+  uint32_t reserved;
+} bsg_params;
+
+/* One chunk: the bytes [offset, offset+len) of a stream, its hashsplit level (trailing zeros
+ * minus split_bits, NOT yet divided by fanout; split/split.go:86 divides) and its ref. */
+typedef struct bsg_chunk {
+  uint64_t offset;
+  uint64_t len;
+  uint32_t level;
+  uint32_t stream;
+  uint8_t ref[32];
+} bsg_chunk; /* 56 bytes */
+
+const char* bsg_errstr(int err);
+bsg_params bsg_params_default(void);
+/* The buzhash32 table used when callers pass table == NULL: rollinghash's GenerateHashes(1). */
+void bsg_default_table(uint32_t out[256]);
+int bsg_device_count(void);
+
+/* ---- streaming split.Writer (bytes arrive from host memory) ---- */
+typedef struct bsg_ctx bsg_ctx;
+bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table /* 256 or NULL */,
+                  int* err);
+/* Copies p[0..n) into pinned staging (the caller keeps ownership of p); full tiles are split
+ * and hashed on the device as they fill. */
+int bsg_write(bsg_ctx* ctx, const uint8_t* p, size_t n);
+/* Flushes the final chunk (hashsplit Splitter.Close). Idempotent. */
+int bsg_close(bsg_ctx* ctx);
+/* Number of finished chunks not yet drained, and drain up to cap of them (stream order). */
+size_t bsg_pending(const bsg_ctx* ctx);
+size_t bsg_drain(bsg_ctx* ctx, bsg_chunk* out, size_t cap);
+/* Staging tile size in bytes (default 256 MiB); call before the first write. */
+int bsg_set_tile(bsg_ctx* ctx, size_t tile_bytes);
+void bsg_free(bsg_ctx* ctx);
+
+/* ---- device-resident batch of independent streams ---- */
+typedef struct bsg_engine bsg_engine;
+bsg_engine* bsg_engine_create(int device, const uint32_t* table /* 256 or NULL */, int* err);
+void bsg_engine_destroy(bsg_engine* eng);
+/* Enqueue split + hash of nstreams streams d_data[off[i] .. off[i]+len[i]) (device memory,
+ * off[i] % 16 == 0; off/len are host arrays). Asynchronous on the engine's stream. */
+int bsg_engine_run(bsg_engine* eng, const uint8_t* d_data, const uint64_t* off,
+                   const uint64_t* len, uint32_t nstreams, const bsg_params* params);
+/* Wait for the run; handles candidate-buffer growth (re-runs once if needed). Returns the
+ * total chunk count in *nchunks. */
+int bsg_engine_finish(bsg_engine* eng, uint64_t* nchunks);
+/* Device pointer to the run's chunk records (stream-major, offset order); valid until the
+ * next run. */
+const bsg_chunk* bsg_engine_chunks_device(const bsg_engine* eng);
+/* Copy records / per-stream counts to host. */
+int bsg_engine_copy_chunks(bsg_engine* eng, bsg_chunk* out, uint64_t cap);
+int bsg_engine_copy_counts(bsg_engine* eng, uint64_t* counts, uint32_t nstreams);
+/* The engine's HIP stream (hipStream_t), e.g. for event timing. */
+void* bsg_engine_stream(bsg_engine* eng);
+/* Per-stage HIP event timing of later runs (enable != 0), and the last finished run's stage
+ * durations in ms: [0] rolling scan (k_scan), [1] prefix/compact/select/chunks, [2] SHA-256
+ * (k_sha). Timed on the engine's own stream. */
+int bsg_engine_profile(bsg_engine* eng, int enable);
+int bsg_engine_stage_ms(const bsg_engine* eng, float out[3]);
+/* Last run's candidate count (diagnostics). */
+uint64_t bsg_engine_candidates(const bsg_engine* eng);
+
+/* Convenience: split + hash host-resident streams (copies to the device), results to host. */
+int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* off,
+                         const uint64_t* len, uint32_t nstreams, const bsg_params* params,
+                         const uint32_t* table, bsg_chunk* out, uint64_t cap, uint64_t* counts,
+                         uint64_t* nchunks);
+
+/* Batched SHA-256 of n blobs base[off[i] .. off[i]+len[i]); base may be host or device memory;
+ * refs receives n*32 bytes (host). */
+int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                     uint32_t n, uint8_t* refs);
+
+/* Utility (benchmarks/tests, not part of the reference surface): fill device memory with the
+ * SplitMix64 counter stream of bs_amd/synth.py (word i = splitmix64(seed + (i+1)*0x9E37...)). */
+int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BSGPU_H */

@@ -1,0 +1,389 @@
+/*
+ * bsoracle.c — CPU ORACLE (test infrastructure only; see bsoracle.h).
+ *
+ * Plain scalar C restatement of the reference's split + ref path. It is the CHECKER for the
+ * HIP path and the "port" CPU baseline in bench.py. It is never linked into libbsgpu.
+ *
+ * Provenance of each piece (the reference is Go; the per-byte loop lives in two third-party
+ * modules that are NOT in /root/reference):
+ *   gorand_*     Go stdlib math/rand rngSource (rng.go: seedrand, Seed, Uint64/Int63) and the
+ *                rngCooked table, which Go generates with gen_cooked.go (ALFG run 7.8e12
+ *                steps from srand(1)). We regenerate rngCooked by polynomial jump-ahead of the
+ *                lagged-Fibonacci recurrence. Pinned: rand.NewSource(1).Int63() must yield
+ *                5577006791947779410, 8674665223082153551, ... (tests/golden/go_rand_kat.json).
+ *   buzhash32_*  github.com/chmduquesne/rollinghash v4.0.0+incompatible, buzhash32:
+ *                GenerateHashes(seed) (uint32(rand.Int63()), skipping duplicates), New() uses
+ *                GenerateHashes(1); Write(window) primes; Roll(c):
+ *                  sum = rotl(sum,1) ^ rotl(T[oldest], len(window) % 32) ^ T[c].   [recalled]
+ *   split_*      github.com/bobg/hashsplit v1.1.1 Splitter: NewSplitter writes 64 zero bytes
+ *                into the buzhash (window 64); Write appends each byte, Rolls it, and once
+ *                len(chunk) >= MinSize checks tz = TrailingZeros32(Sum32()); tz >= SplitBits
+ *                => emit (chunk, level = tz - SplitBits), chunk = nil, no reset (Reset=false).
+ *                Close emits the non-empty remainder with level from the same check (0 if the
+ *                check fails).                                                      [recalled]
+ *                BS wiring: split/split.go:85-89 (callback, MinSize 1024, SplitBits 16).
+ *   sha256       FIPS 180-4; bs.Blob.Ref (bs.go:24-26) = crypto/sha256.Sum256.
+ */
+#include "bsoracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------
+ * Go math/rand (rngSource) restatement.
+ * ---------------------------------------------------------------------------------------- */
+#define RNG_LEN 607
+#define RNG_TAP 273
+#define INT32MAX 2147483647
+
+static int32_t gorand_seedrand(int32_t x) { /* x[n+1] = 48271 * x[n] mod (2**31 - 1) */
+    const int32_t A = 48271, Q = 44488, R = 3399;
+    int32_t hi = x / Q, lo = x % Q;
+    x = A * lo - R * hi;
+    if (x < 0) x += INT32MAX;
+    return x;
+}
+
+/* p(x) = x^607 - x^334 - 1 over Z/2^64: the characteristic polynomial of
+ * y[n] = y[n-607] + y[n-273] (the ALFG output sequence). out = a*b mod p. */
+static void gorand_polymulmod(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+    uint64_t t[2 * RNG_LEN];
+    memset(t, 0, sizeof t);
+    for (int i = 0; i < RNG_LEN; i++) {
+        if (!a[i]) continue;
+        for (int j = 0; j < RNG_LEN; j++) t[i + j] += a[i] * b[j];
+    }
+    for (int k = 2 * RNG_LEN - 2; k >= RNG_LEN; k--) {
+        uint64_t c = t[k];
+        if (!c) continue;
+        t[k] = 0;
+        t[k - RNG_LEN + 334] += c;
+        t[k - RNG_LEN] += c;
+    }
+    memcpy(out, t, RNG_LEN * sizeof(uint64_t));
+}
+
+static uint64_t g_cooked[RNG_LEN];
+static int g_cooked_ready;
+static pthread_mutex_t g_cooked_mu = PTHREAD_MUTEX_INITIALIZER;
+
+/* gen_cooked.go: srand(1) with (<<20, <<10) mixing, then 7.8e12 vrand() calls; rngCooked is
+ * the resulting 607-word feedback register. Computed here by jump-ahead (milliseconds). */
+static void gorand_make_cooked(void) {
+    pthread_mutex_lock(&g_cooked_mu);
+    if (g_cooked_ready) { pthread_mutex_unlock(&g_cooked_mu); return; }
+    uint64_t vec[RNG_LEN];
+    int tap = 0, feed = RNG_LEN - RNG_TAP;
+    int32_t x = 1;
+    for (int i = -20; i < RNG_LEN; i++) {
+        x = gorand_seedrand(x);
+        if (i >= 0) {
+            uint64_t u = (uint64_t)(int64_t)x << 20;
+            x = gorand_seedrand(x);
+            u ^= (uint64_t)(int64_t)x << 10;
+            x = gorand_seedrand(x);
+            u ^= (uint64_t)(int64_t)x;
+            vec[i] = u;
+        }
+    }
+    uint64_t y[RNG_LEN]; /* first 607 outputs: the basis of the recurrence */
+    for (int i = 0; i < RNG_LEN; i++) {
+        if (--tap < 0) tap += RNG_LEN;
+        if (--feed < 0) feed += RNG_LEN;
+        vec[feed] += vec[tap];
+        y[i] = vec[feed];
+    }
+    const uint64_t M = 7800000000000ULL; /* calls made by gen_cooked.go */
+    uint64_t e = M - RNG_LEN;
+    uint64_t c[RNG_LEN], b[RNG_LEN], tmp[RNG_LEN];
+    memset(c, 0, sizeof c); c[0] = 1;  /* c = x^0 */
+    memset(b, 0, sizeof b); b[1] = 1;  /* b = x^1 */
+    while (e) {
+        if (e & 1) { gorand_polymulmod(c, b, tmp); memcpy(c, tmp, sizeof c); }
+        e >>= 1;
+        if (e) { gorand_polymulmod(b, b, tmp); memcpy(b, tmp, sizeof b); }
+    }
+    /* outputs M-607 .. M-1; output n was stored at vec[(334 - (n+1)) mod 607] */
+    for (int j = 0; j < RNG_LEN; j++) {
+        uint64_t v = 0;
+        for (int i = 0; i < RNG_LEN; i++) v += c[i] * y[i];
+        uint64_t n = M - RNG_LEN + (uint64_t)j;
+        int idx = (int)(((int64_t)334 - (int64_t)((n + 1) % RNG_LEN) + 2 * RNG_LEN) % RNG_LEN);
+        g_cooked[idx] = v;
+        uint64_t top = c[RNG_LEN - 1]; /* c *= x (mod p) */
+        memmove(c + 1, c, (RNG_LEN - 1) * sizeof(uint64_t));
+        c[0] = top;
+        c[334] += top;
+    }
+    g_cooked_ready = 1;
+    pthread_mutex_unlock(&g_cooked_mu);
+}
+
+typedef struct { int tap, feed; uint64_t vec[RNG_LEN]; } gorand_src;
+
+static void gorand_src_seed(gorand_src* r, int64_t seed) { /* rng.go rngSource.Seed */
+    gorand_make_cooked();
+    r->tap = 0;
+    r->feed = RNG_LEN - RNG_TAP;
+    seed = seed % INT32MAX;
+    if (seed < 0) seed += INT32MAX;
+    if (seed == 0) seed = 89482311;
+    int32_t x = (int32_t)seed;
+    for (int i = -20; i < RNG_LEN; i++) {
+        x = gorand_seedrand(x);
+        if (i >= 0) {
+            uint64_t u = (uint64_t)(int64_t)x << 40;
+            x = gorand_seedrand(x);
+            u ^= (uint64_t)(int64_t)x << 20;
+            x = gorand_seedrand(x);
+            u ^= (uint64_t)(int64_t)x;
+            u ^= g_cooked[i];
+            r->vec[i] = u;
+        }
+    }
+}
+
+static int64_t gorand_src_int63(gorand_src* r) { /* rngSource.Uint64() & rngMask */
+    if (--r->tap < 0) r->tap += RNG_LEN;
+    if (--r->feed < 0) r->feed += RNG_LEN;
+    uint64_t x = r->vec[r->feed] + r->vec[r->tap];
+    r->vec[r->feed] = x;
+    return (int64_t)(x & 0x7fffffffffffffffULL);
+}
+
+static gorand_src g_src;
+void bso_gorand_seed(int64_t seed) { gorand_src_seed(&g_src, seed); }
+int64_t bso_gorand_int63(void) { return gorand_src_int63(&g_src); }
+
+/* ------------------------------------------------------------------------------------------
+ * buzhash32 (rollinghash v4.0.0) restatement.
+ * ---------------------------------------------------------------------------------------- */
+void bso_buzhash32_generate(int64_t seed, uint32_t out[256]) { /* GenerateHashes(seed) */
+    gorand_src r;
+    gorand_src_seed(&r, seed);
+    for (int i = 0; i < 256; i++) {
+        uint32_t x;
+        for (;;) { /* `for used[x] { x = uint32(random.Int63()) }` */
+            x = (uint32_t)gorand_src_int63(&r);
+            int dup = 0;
+            for (int j = 0; j < i; j++) dup |= (out[j] == x);
+            if (!dup) break;
+        }
+        out[i] = x;
+    }
+}
+
+static inline uint32_t rotl32(uint32_t x, unsigned r) {
+    r &= 31;
+    return r ? (x << r) | (x >> (32 - r)) : x;
+}
+
+typedef struct { /* Buzhash32 with a 64-byte window */
+    uint32_t sum;
+    uint8_t window[64];
+    int oldest;
+    unsigned nrotate; /* len(window) % 32 */
+    const uint32_t* T;
+} buzhash32;
+
+static void buzhash32_init_zero(buzhash32* d, const uint32_t* T) {
+    /* NewSplitter: rs := buzhash32.New(); rs.Write(zeroes[:64]) */
+    d->T = T;
+    d->sum = 0;
+    memset(d->window, 0, sizeof d->window);
+    d->oldest = 0;
+    for (int i = 0; i < 64; i++) d->sum = rotl32(d->sum, 1) ^ T[0];
+    d->nrotate = 64 % 32;
+}
+
+static inline void buzhash32_roll(buzhash32* d, uint8_t c) {
+    uint32_t hn = d->T[c];
+    uint32_t h0 = d->T[d->window[d->oldest]];
+    d->window[d->oldest] = c;
+    if (++d->oldest >= 64) d->oldest = 0;
+    d->sum = rotl32(d->sum, 1) ^ rotl32(h0, d->nrotate) ^ hn;
+}
+
+void bso_rolling_sums(const uint32_t table[256], const uint8_t* x, size_t n, uint32_t* out) {
+    buzhash32 d;
+    buzhash32_init_zero(&d, table);
+    for (size_t p = 0; p < n; p++) {
+        buzhash32_roll(&d, x[p]);
+        out[p] = d.sum;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * SHA-256, FIPS 180-4 §6.2.
+ * ---------------------------------------------------------------------------------------- */
+static const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+static inline uint32_t rotr32(uint32_t x, unsigned r) { return (x >> r) | (x << (32 - r)); }
+
+static void sha256_block(uint32_t st[8], const uint8_t* p) {
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++)
+        w[i] = ((uint32_t)p[4 * i] << 24) | ((uint32_t)p[4 * i + 1] << 16) |
+               ((uint32_t)p[4 * i + 2] << 8) | p[4 * i + 3];
+    for (int i = 16; i < 64; i++) {
+        uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    for (int i = 0; i < 64; i++) {
+        uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+        uint32_t ch = (e & f) ^ (~e & g);
+        uint32_t t1 = h + S1 + ch + K256[i] + w[i];
+        uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        uint32_t t2 = S0 + mj;
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+void bso_sha256(const uint8_t* data, size_t n, uint8_t out[32]) {
+    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    size_t full = n / 64;
+    for (size_t i = 0; i < full; i++) sha256_block(st, data + 64 * i);
+    uint8_t tail[128];
+    size_t r = n - 64 * full;
+    memset(tail, 0, sizeof tail);
+    memcpy(tail, data + 64 * full, r);
+    tail[r] = 0x80;
+    size_t tl = (r + 9 <= 64) ? 64 : 128;
+    uint64_t bits = (uint64_t)n * 8;
+    for (int i = 0; i < 8; i++) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    sha256_block(st, tail);
+    if (tl == 128) sha256_block(st, tail + 64);
+    for (int i = 0; i < 8; i++) {
+        out[4 * i] = (uint8_t)(st[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+        out[4 * i + 3] = (uint8_t)st[i];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * hashsplit.Splitter restatement (one stream).
+ * ---------------------------------------------------------------------------------------- */
+static inline unsigned tz32(uint32_t h) { return h ? (unsigned)__builtin_ctz(h) : 32u; }
+
+static void emit(bso_chunk* out, size_t cap, size_t k, const uint8_t* x, uint64_t start,
+                 uint64_t len, unsigned level, int with_refs, uint32_t stream) {
+    if (k >= cap) return;
+    out[k].offset = start;
+    out[k].len = len;
+    out[k].level = level;
+    out[k].stream = stream;
+    if (with_refs) bso_sha256(x + start, (size_t)len, out[k].ref);
+    else memset(out[k].ref, 0, 32);
+}
+
+static size_t split_one(const uint32_t table[256], const uint8_t* x, size_t n, unsigned split_bits,
+                        unsigned min_size, int with_refs, bso_chunk* out, size_t cap,
+                        uint32_t stream) {
+    buzhash32 d;
+    buzhash32_init_zero(&d, table);
+    if (min_size == 0) min_size = 64; /* hashsplit defaultMinSize = windowSize */
+    if (split_bits == 0) split_bits = 13; /* hashsplit defaultSplitBits */
+    size_t k = 0;
+    uint64_t start = 0;
+    for (size_t p = 0; p < n; p++) {
+        buzhash32_roll(&d, x[p]);              /* s.chunk = append(s.chunk, c); s.rs.Roll(c) */
+        uint64_t len = (uint64_t)p + 1 - start;
+        if (len < min_size) continue;          /* if len(s.chunk) < minSize { continue } */
+        unsigned tz = tz32(d.sum);             /* checkSplit */
+        if (tz >= split_bits) {
+            emit(out, cap, k, x, start, len, tz - split_bits, with_refs, stream);
+            k++;
+            start = (uint64_t)p + 1;           /* s.chunk = nil; Reset=false: no re-prime */
+        }
+    }
+    if (start < n) {                           /* Close(): flush the remainder */
+        unsigned tz = tz32(d.sum);
+        unsigned level = (tz >= split_bits) ? tz - split_bits : 0;
+        emit(out, cap, k, x, start, (uint64_t)n - start, level, with_refs, stream);
+        k++;
+    }
+    return k;
+}
+
+size_t bso_split(const uint32_t table[256], const uint8_t* x, size_t n, unsigned split_bits,
+                 unsigned min_size, int with_refs, bso_chunk* out, size_t cap) {
+    return split_one(table, x, n, split_bits, min_size, with_refs, out, cap, 0);
+}
+
+/* ---- multi-stream, multi-threaded (one stream per task; the reference is one goroutine per
+ * stream, split/split.go:30-37 has no internal parallelism) ---- */
+typedef struct {
+    const uint32_t* table;
+    const uint8_t* base;
+    const uint64_t* off;
+    const uint64_t* len;
+    uint32_t nstreams;
+    unsigned bits, min_size;
+    bso_chunk** tmp;
+    size_t* cnt;
+    uint32_t next;
+    pthread_mutex_t mu;
+} mt_job;
+
+static void* mt_worker(void* arg) {
+    mt_job* j = (mt_job*)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        uint32_t s = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (s >= j->nstreams) break;
+        const uint8_t* x = j->base + j->off[s];
+        size_t n = (size_t)j->len[s];
+        size_t c = split_one(j->table, x, n, j->bits, j->min_size, 0, NULL, 0, s);
+        bso_chunk* buf = (bso_chunk*)malloc((c ? c : 1) * sizeof(bso_chunk));
+        split_one(j->table, x, n, j->bits, j->min_size, 1, buf, c, s);
+        j->tmp[s] = buf;
+        j->cnt[s] = c;
+    }
+    return NULL;
+}
+
+size_t bso_split_streams(const uint32_t table[256], const uint8_t* base, const uint64_t* off,
+                         const uint64_t* len, uint32_t nstreams, unsigned split_bits,
+                         unsigned min_size, int threads, bso_chunk* out, size_t cap,
+                         uint64_t* counts) {
+    mt_job j;
+    j.table = table; j.base = base; j.off = off; j.len = len; j.nstreams = nstreams;
+    j.bits = split_bits; j.min_size = min_size; j.next = 0;
+    j.tmp = (bso_chunk**)calloc(nstreams ? nstreams : 1, sizeof(bso_chunk*));
+    j.cnt = (size_t*)calloc(nstreams ? nstreams : 1, sizeof(size_t));
+    pthread_mutex_init(&j.mu, NULL);
+    gorand_make_cooked(); /* not needed, but keeps first-call latency out of workers */
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, mt_worker, &j);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    size_t total = 0;
+    for (uint32_t s = 0; s < nstreams; s++) {
+        if (counts) counts[s] = j.cnt[s];
+        for (size_t i = 0; i < j.cnt[s]; i++) {
+            if (total < cap) out[total] = j.tmp[s][i];
+            total++;
+        }
+        free(j.tmp[s]);
+    }
+    free(th); free(j.tmp); free(j.cnt);
+    pthread_mutex_destroy(&j.mu);
+    return total;
+}

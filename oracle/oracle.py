@@ -1,0 +1,201 @@
+"""CPU ORACLE — test infrastructure only.
+
+ctypes wrapper over oracle/libbsoracle.so (the C restatement in bsoracle.c) plus a pure-Python
+restatement (`py_split`, `py_rolling_sums`) used to cross-check the C one on small inputs.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker. The product path (bs_amd/) never imports it.
+
+Reference anchors: split/split.go:85-89 (Splitter wiring + defaults), bs.go:24-26 (ref =
+SHA-256). The Splitter / buzhash32 semantics are restated from github.com/bobg/hashsplit v1.1.1
+and github.com/chmduquesne/rollinghash v4.0.0 (not in /root/reference; see bsoracle.c).
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libbsoracle.so")
+
+
+class Chunk(ctypes.Structure):
+    _fields_ = [
+        ("offset", ctypes.c_uint64),
+        ("len", ctypes.c_uint64),
+        ("level", ctypes.c_uint32),
+        ("stream", ctypes.c_uint32),
+        ("ref", ctypes.c_uint8 * 32),
+    ]
+
+
+CHUNK_DTYPE = np.dtype(
+    [("offset", "<u8"), ("len", "<u8"), ("level", "<u4"), ("stream", "<u4"), ("ref", "u1", (32,))]
+)
+assert CHUNK_DTYPE.itemsize == ctypes.sizeof(Chunk) == 56
+
+
+def build() -> str:
+    """Compile the oracle (gcc) in place; returns the .so path."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.bso_gorand_seed.argtypes = [ctypes.c_int64]
+        L.bso_gorand_int63.restype = ctypes.c_int64
+        L.bso_buzhash32_generate.argtypes = [ctypes.c_int64, u32p]
+        L.bso_rolling_sums.argtypes = [u32p, u8p, ctypes.c_size_t, u32p]
+        L.bso_sha256.argtypes = [u8p, ctypes.c_size_t, u8p]
+        L.bso_split.restype = ctypes.c_size_t
+        L.bso_split.argtypes = [u32p, u8p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint,
+                                ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        L.bso_split_streams.restype = ctypes.c_size_t
+        L.bso_split_streams.argtypes = [u32p, u8p, u64p, u64p, ctypes.c_uint32, ctypes.c_uint,
+                                        ctypes.c_uint, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_size_t, u64p]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def gorand_int63(seed: int, n: int) -> list[int]:
+    L = lib()
+    L.bso_gorand_seed(seed)
+    return [L.bso_gorand_int63() for _ in range(n)]
+
+
+def buzhash32_table(seed: int = 1) -> np.ndarray:
+    t = np.zeros(256, dtype=np.uint32)
+    lib().bso_buzhash32_generate(seed, _p(t, ctypes.c_uint32))
+    return t
+
+
+def rolling_sums(table: np.ndarray, data: bytes | np.ndarray) -> np.ndarray:
+    x = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    out = np.zeros(len(x), dtype=np.uint32)
+    t = np.ascontiguousarray(table, dtype=np.uint32)
+    lib().bso_rolling_sums(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x),
+                           _p(out, ctypes.c_uint32))
+    return out
+
+
+def sha256(data: bytes | np.ndarray) -> bytes:
+    x = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8))
+    out = np.zeros(32, dtype=np.uint8)
+    lib().bso_sha256(_p(x, ctypes.c_uint8), len(x), _p(out, ctypes.c_uint8))
+    return out.tobytes()
+
+
+def split(table: np.ndarray, data, bits: int = 16, min_size: int = 1024,
+          with_refs: bool = True) -> np.ndarray:
+    """Chunks of one stream as a CHUNK_DTYPE array (offset, len, level, stream=0, ref)."""
+    x = data if isinstance(data, np.ndarray) else np.frombuffer(bytes(data), dtype=np.uint8)
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    t = np.ascontiguousarray(table, dtype=np.uint32)
+    L = lib()
+    n = L.bso_split(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits, min_size, 0,
+                    None, 0)
+    out = np.zeros(max(n, 1), dtype=CHUNK_DTYPE)
+    L.bso_split(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits, min_size,
+                int(with_refs), out.ctypes.data, n)
+    return out[:n]
+
+
+def split_streams(table: np.ndarray, base: np.ndarray, off, lens, bits: int = 16,
+                  min_size: int = 1024, threads: int = 1) -> tuple[np.ndarray, np.ndarray]:
+    """Multi-stream split+ref (threads = worker threads). Returns (chunks, counts)."""
+    t = np.ascontiguousarray(table, dtype=np.uint32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    counts = np.zeros(len(off), dtype=np.uint64)
+    cap = int(sum(int(l) // max(min_size, 64) + 1 for l in lens))
+    out = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
+    n = lib().bso_split_streams(_p(t, ctypes.c_uint32), _p(base, ctypes.c_uint8),
+                                _p(off, ctypes.c_uint64), _p(lens, ctypes.c_uint64), len(off),
+                                bits, min_size, threads, out.ctypes.data, cap,
+                                _p(counts, ctypes.c_uint64))
+    assert n <= cap
+    return out[:n], counts
+
+
+# ---------------------------------------------------------------------------------------------
+# Pure-Python restatement (small inputs only): literal Splitter + Buzhash32 loop.
+# ---------------------------------------------------------------------------------------------
+def _rotl(x: int, r: int) -> int:
+    r &= 31
+    return ((x << r) | (x >> (32 - r))) & 0xFFFFFFFF if r else x
+
+
+def py_rolling_sums(table, data: bytes) -> list[int]:
+    T = [int(v) for v in table]
+    window = [0] * 64          # rs.Write(64 zero bytes)
+    s = 0
+    for _ in range(64):
+        s = _rotl(s, 1) ^ T[0]
+    oldest = 0
+    out = []
+    for c in data:             # Roll(c)
+        h0 = T[window[oldest]]
+        window[oldest] = c
+        oldest = (oldest + 1) % 64
+        s = _rotl(s, 1) ^ _rotl(h0, 64 % 32) ^ T[c]
+        out.append(s)
+    return out
+
+
+def py_window_hash(table, data: bytes, p: int) -> int:
+    """Closed form h(p) = XOR_{k<64} rotl(T[x[p-k]], k mod 32), x[j<0] = 0."""
+    T = [int(v) for v in table]
+    h = 0
+    for k in range(64):
+        j = p - k
+        h ^= _rotl(T[data[j] if j >= 0 else 0], k % 32)
+    return h
+
+
+@dataclass
+class PyChunk:
+    offset: int
+    len: int
+    level: int
+    ref: bytes
+
+
+def py_split(table, data: bytes, bits: int = 16, min_size: int = 1024) -> list[PyChunk]:
+    sums = py_rolling_sums(table, data)
+    out, start = [], 0
+    for p, h in enumerate(sums):
+        if p + 1 - start < min_size:
+            continue
+        tz = (h & -h).bit_length() - 1 if h else 32
+        if tz >= bits:
+            out.append(PyChunk(start, p + 1 - start, tz - bits,
+                               hashlib.sha256(data[start:p + 1]).digest()))
+            start = p + 1
+    if start < len(data):
+        h = sums[-1]
+        tz = (h & -h).bit_length() - 1 if h else 32
+        out.append(PyChunk(start, len(data) - start, tz - bits if tz >= bits else 0,
+                           hashlib.sha256(data[start:]).digest()))
+    return out

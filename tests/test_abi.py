@@ -1,0 +1,51 @@
+"""C-ABI library: builds, loads, exports every symbol include/bsgpu.h declares (no GPU needed)."""
+import ctypes
+import subprocess
+
+import numpy as np
+
+from conftest import GOLD
+
+
+def test_library_builds_and_exports_header_symbols():
+    from bs_amd import build, bsgpu
+    path = build.build()
+    declared = bsgpu.exported_symbols_from_header()
+    assert len(declared) >= 20
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    L = bsgpu.lib()
+    for s in declared:
+        assert hasattr(L, s)
+
+
+def test_struct_layout_and_defaults():
+    from bs_amd import bsgpu
+    from oracle.oracle import CHUNK_DTYPE as ORACLE_DTYPE
+    assert bsgpu.CHUNK_DTYPE == ORACLE_DTYPE
+    p = bsgpu.lib().bsg_params_default()
+    assert (p.split_bits, p.min_size, p.fanout) == (16, 1024, 8)  # split/split.go:48,88-89
+    assert ctypes.sizeof(bsgpu.Params) == 16
+
+
+def test_default_table_matches_golden():
+    from bs_amd import bsgpu
+    golden = np.fromfile(f"{GOLD}/buzhash32_table.bin", dtype="<u4")
+    assert bsgpu.default_table().tolist() == golden.tolist()
+
+
+def test_errstr_and_bad_device():
+    from bs_amd import bsgpu
+    L = bsgpu.lib()
+    assert L.bsg_errstr(0) == b"ok"
+    assert L.bsg_errstr(-22) == b"invalid argument"
+    err = ctypes.c_int(0)
+    n = L.bsg_device_count()
+    h = L.bsg_open(n + 3, None, None, ctypes.byref(err))  # no such device
+    assert not h and err.value == -19
+    bad = bsgpu.Params(16, 32, 8, 0)  # MinSize below the 64-byte window
+    h = L.bsg_open(0, ctypes.byref(bad), None, ctypes.byref(err))
+    assert not h and err.value == -22

@@ -1,0 +1,213 @@
+"""HIP path (through the C ABI) vs the CPU oracle and the golden fixtures — bit-exact.
+
+Mirrors the reference's own split tests (split/split_test.go:15-108: empty input, Bits(4)
+round trip over yubnub.opus) and the store harness (testutil/readwrite.go:18-54), but compares
+chunk boundaries, levels and refs exactly instead of only round-tripping.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_json, read_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def as_tuples(ch):
+    return [(int(c["offset"]), int(c["len"]), int(c["level"]), bytes(c["ref"]).hex()) for c in ch]
+
+
+def golden_tuples(v):
+    return list(zip(v["offset"], v["len"], v["level"], v["ref"]))
+
+
+def _vector_input(key):
+    from bs_amd.synth import splitmix_bytes
+    if key.startswith("splitmix:"):
+        _, seed, n = key.split(":")
+        return splitmix_bytes(0xB5B52026 + int(seed), int(n))
+    return read_golden(key)
+
+
+# --------------------------------------------------------------------------------------------
+# SHA-256
+# --------------------------------------------------------------------------------------------
+def test_sha256_batch_kats(gpu):
+    kat = load_json("sha256_kat.json")
+    from bs_amd.synth import splitmix_bytes
+    pat = splitmix_bytes(kat["pattern_seed"], 1100)
+    blobs = [pat[:n] for n in range(1101)]
+    got = gpu.sha256_batch(blobs)
+    assert [g.hex() for g in got] == kat["pattern_digests"]
+    fips = list(kat["fips"].items())
+    got = gpu.sha256_batch([m.encode() for m, _ in fips] + [b"a" * 1000000])
+    assert [g.hex() for g in got] == [d for _, d in fips] + [kat["million_a"]]
+    names = list(kat["files"])
+    got = gpu.sha256_batch([read_golden(n) for n in names])
+    assert [g.hex() for g in got] == [kat["files"][n] for n in names]
+
+
+# --------------------------------------------------------------------------------------------
+# Split + ref, batch API
+# --------------------------------------------------------------------------------------------
+def test_split_empty(gpu):
+    """split_test.go:15-25 TestSplitEmpty: no input, no chunks."""
+    ch, counts = gpu.split_hash_batch([b""])
+    assert len(ch) == 0 and counts.tolist() == [0]
+
+
+def test_chunker_kats_table_independent(gpu, table):
+    kat = load_json("chunker_kat.json")
+    unit = bytes.fromhex(kat["period32_unit"])
+    rng = np.random.default_rng(1)
+    rnd_table = rng.integers(0, 2**32, size=256, dtype=np.uint64).astype(np.uint32)
+    for c in kat["cases"]:
+        n = c["n"]
+        data = bytes(n) if c["name"].startswith("zeros") else (unit * (n // 32 + 1))[:n]
+        for t in (table, rnd_table):
+            ch, _ = gpu.split_hash_batch([data], bits=c["bits"], min_size=c["min_size"], table=t)
+            assert as_tuples(ch) == golden_tuples(c), (c["name"], c["bits"], c["min_size"])
+
+
+def test_split_vectors_golden(gpu):
+    for v in load_json("split_vectors.json")["vectors"]:
+        data = _vector_input(v["input"])
+        ch, _ = gpu.split_hash_batch([data], bits=v["bits"], min_size=v["min_size"])
+        assert as_tuples(ch) == golden_tuples(v), (v["input"], v["bits"], v["min_size"])
+
+
+def test_testsplit_bits4_yubnub(gpu, oracle, table):
+    """split_test.go:27-31 configuration (Bits(4), default MinSize) + byte round trip."""
+    data = read_golden("yubnub.opus")
+    ch, _ = gpu.split_hash_batch([data], bits=4)
+    ref = oracle.split(table, data, bits=4, min_size=1024)
+    assert as_tuples(ch) == as_tuples(ref)
+    rebuilt = b"".join(data[int(c["offset"]):int(c["offset"] + c["len"])] for c in ch)
+    assert rebuilt == data
+    for c in ch[:50]:
+        o, n = int(c["offset"]), int(c["len"])
+        assert bytes(c["ref"]) == hashlib.sha256(data[o:o + n]).digest()
+
+
+EDGE_LENS = [0, 1, 2, 63, 64, 65, 127, 128, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096,
+             4097, 65535, 65536, 65537, 131072 + 7]
+
+
+@pytest.mark.parametrize("bits,min_size", [(16, 1024), (13, 64), (8, 64), (4, 1024), (20, 4096),
+                                           (1, 64), (32, 64)])
+def test_multistream_random_vs_oracle(gpu, oracle, table, bits, min_size):
+    from bs_amd.synth import splitmix_array
+    rng = np.random.default_rng(bits * 1000 + min_size)
+    lens = EDGE_LENS + [int(x) for x in rng.integers(0, 300_000, size=12)]
+    arrs = [splitmix_array(1000 + i, n) for i, n in enumerate(lens)]
+    ch, counts = gpu.split_hash_batch(arrs, bits=bits, min_size=min_size)
+    k = 0
+    for i, a in enumerate(arrs):
+        one = oracle.split(table, a, bits=bits, min_size=min_size)
+        got = ch[k:k + int(counts[i])]
+        assert int(counts[i]) == len(one), (i, len(a))
+        assert as_tuples(got) == as_tuples(one), (i, len(a))
+        assert (got["stream"] == i).all()
+        k += int(counts[i])
+    assert k == len(ch)
+
+
+def test_dense_candidates_zero_runs(gpu, oracle, table):
+    """Long zero runs inside random data: every position in the run is a candidate."""
+    from bs_amd.synth import splitmix_array
+    a = splitmix_array(77, 500_000)
+    a[100_000:300_000] = 0
+    a[400_000:400_100] = 0
+    for bits, mn in ((16, 1024), (12, 64)):
+        ch, _ = gpu.split_hash_batch([a], bits=bits, min_size=mn)
+        assert as_tuples(ch) == as_tuples(oracle.split(table, a, bits=bits, min_size=mn))
+
+
+# --------------------------------------------------------------------------------------------
+# Streaming split.Writer path: arbitrary Write sizes, tiles carried across segments
+# --------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("tile", [4096, 5000, 65536 + 3, 1 << 20])
+def test_streaming_writer_vs_oracle(gpu, oracle, table, tile):
+    from bs_amd.synth import splitmix_bytes
+    data = splitmix_bytes(4242, 3_000_017)
+    data = data[:1_500_000] + bytes(70_000) + data[1_500_000:]  # a dense stretch
+    rng = np.random.default_rng(tile)
+    for bits, mn in ((16, 1024), (10, 64)):
+        w = gpu.StreamingSplitter(bits=bits, min_size=mn, tile=tile)
+        pos, got = 0, []
+        while pos < len(data):
+            k = int(rng.choice([1, 7, 100, 4096, 32768, 300_000]))
+            w.write(data[pos:pos + k])
+            pos += k
+            got.append(w.drain())
+        w.close()
+        got.append(w.drain())
+        w.free()
+        ch = np.concatenate(got)
+        assert as_tuples(ch) == as_tuples(oracle.split(table, data, bits=bits, min_size=mn))
+
+
+def test_streaming_small_and_empty(gpu, oracle, table):
+    for n in (0, 1, 63, 64, 1023, 1024, 1025, 4095, 4096, 4097):
+        from bs_amd.synth import splitmix_bytes
+        d = splitmix_bytes(n, n)
+        w = gpu.StreamingSplitter(bits=8, min_size=64, tile=4096)
+        w.write(d)
+        w.close()
+        ch = w.drain()
+        w.free()
+        assert as_tuples(ch) == as_tuples(oracle.split(table, d, bits=8, min_size=64)), n
+
+
+# --------------------------------------------------------------------------------------------
+# Device-resident engine (the bench path) at full size
+# --------------------------------------------------------------------------------------------
+def _device_stream_run(gpu, nbytes_list, seed0, bits=16, min_size=1024):
+    import torch
+    offs, total = [], 0
+    for n in nbytes_list:
+        offs.append(total)
+        total += (n + 15) & ~15
+    buf = torch.empty(max(total, 16), dtype=torch.uint8, device="cuda")
+    eng = gpu.Engine()
+    for i, (o, n) in enumerate(zip(offs, nbytes_list)):
+        gpu.fill_splitmix(buf.data_ptr() + o, n, seed0 + i, stream=eng.stream)
+    eng.run(buf.data_ptr(), offs, nbytes_list, bits=bits, min_size=min_size)
+    eng.finish()
+    return eng, buf, offs
+
+
+def test_engine_device_resident_vs_oracle(gpu, oracle, table):
+    from bs_amd.synth import splitmix_array
+    lens = [64 << 20, 3_000_001, 0, 17]
+    eng, buf, offs = _device_stream_run(gpu, lens, 0xB5B52026)
+    ch = eng.chunks()
+    counts = eng.counts()
+    k = 0
+    for i, n in enumerate(lens):
+        host = splitmix_array(0xB5B52026 + i, n)
+        dev = buf[offs[i]:offs[i] + n].cpu().numpy()
+        assert np.array_equal(host, dev)  # device generator == host generator
+        one = oracle.split(table, host)
+        assert as_tuples(ch[k:k + int(counts[i])]) == as_tuples(one)
+        k += int(counts[i])
+    eng.close()
+
+
+@pytest.mark.slow
+def test_engine_1gib_full_parity(gpu, oracle, table):
+    """BASELINE config 2 (1 GiB random stream, default params): full oracle comparison."""
+    from bs_amd.synth import splitmix_array
+    n = 1 << 30
+    eng, buf, offs = _device_stream_run(gpu, [n], 0xB5B52026)
+    ch = eng.chunks()
+    host = splitmix_array(0xB5B52026, n)
+    one = oracle.split(table, host)
+    assert len(ch) == len(one)
+    assert (ch["offset"] == one["offset"]).all() and (ch["len"] == one["len"]).all()
+    assert (ch["level"] == one["level"]).all() and (ch["ref"] == one["ref"]).all()
+    # size-independent properties
+    assert int(ch["len"].sum()) == n
+    assert (ch["len"][:-1] >= 1024).all()
+    eng.close()

@@ -1,0 +1,112 @@
+"""CPU oracle pinned against the committed golden fixtures (no GPU)."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_json, read_golden
+
+
+def test_go_rand_known_answers(oracle):
+    kat = load_json("go_rand_kat.json")
+    assert oracle.gorand_int63(kat["seed"], len(kat["int63"])) == kat["int63"]
+
+
+def test_default_table_is_generatehashes_1(oracle, table):
+    t = oracle.buzhash32_table(1)
+    assert t.tolist() == table.tolist()
+    assert len(set(t.tolist())) == 256
+
+
+def test_sha256_kats(oracle):
+    kat = load_json("sha256_kat.json")
+    for msg, dig in kat["fips"].items():
+        assert oracle.sha256(msg.encode()).hex() == dig
+    assert oracle.sha256(b"a" * 1000000).hex() == kat["million_a"]
+    from bs_amd.synth import splitmix_bytes
+    pat = splitmix_bytes(kat["pattern_seed"], 1100)
+    for n, d in enumerate(kat["pattern_digests"]):
+        assert oracle.sha256(pat[:n]).hex() == d, n
+    for name, d in kat["files"].items():
+        assert oracle.sha256(read_golden(name)).hex() == d
+
+
+def test_rolling_closed_form_matches_roll(oracle, table):
+    from bs_amd.synth import splitmix_bytes
+    d = splitmix_bytes(7, 3000)
+    sums = oracle.rolling_sums(table, d)
+    for p in [0, 1, 31, 62, 63, 64, 65, 127, 128, 1000, 2999]:
+        assert oracle.py_window_hash(table, d, p) == int(sums[p])
+
+
+def test_period32_windows_hash_to_zero(oracle):
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        t = rng.integers(0, 2**32, size=256, dtype=np.uint64).astype(np.uint32)
+        unit = rng.integers(0, 256, size=32, dtype=np.uint8).tobytes()
+        sums = oracle.rolling_sums(t, unit * 10)
+        assert (sums[63:] == 0).all()
+        assert (oracle.rolling_sums(t, bytes(500)) == 0).all()
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_chunker_kats_table_independent(oracle, table, case):
+    kat = load_json("chunker_kat.json")
+    c = kat["cases"][case]
+    unit = bytes.fromhex(kat["period32_unit"])
+    n = c["n"]
+    data = bytes(n) if c["name"].startswith("zeros") else (unit * (n // 32 + 1))[:n]
+    rng = np.random.default_rng(case)
+    for t in (table, rng.integers(0, 2**32, size=256, dtype=np.uint64).astype(np.uint32)):
+        ch = oracle.split(t, data, bits=c["bits"], min_size=c["min_size"])
+        assert ch["offset"].tolist() == c["offset"]
+        assert ch["len"].tolist() == c["len"]
+        assert ch["level"].tolist() == c["level"]
+        assert [bytes(r).hex() for r in ch["ref"]] == c["ref"]
+
+
+def _vector_input(key):
+    from bs_amd.synth import splitmix_bytes
+    if key.startswith("splitmix:"):
+        _, seed, n = key.split(":")
+        return splitmix_bytes(0xB5B52026 + int(seed), int(n))
+    return read_golden(key)
+
+
+def test_split_vectors(oracle, table):
+    for v in load_json("split_vectors.json")["vectors"]:
+        data = _vector_input(v["input"])
+        ch = oracle.split(table, data, bits=v["bits"], min_size=v["min_size"])
+        assert ch["offset"].tolist() == v["offset"], v["input"]
+        assert ch["len"].tolist() == v["len"]
+        assert ch["level"].tolist() == v["level"]
+        assert [bytes(r).hex() for r in ch["ref"]] == v["ref"]
+
+
+def test_python_and_c_restatements_agree(oracle, table):
+    from bs_amd.synth import splitmix_bytes
+    for seed, n, bits, mn in [(11, 70_000, 8, 64), (12, 5000, 4, 64), (13, 200, 4, 64),
+                              (14, 64, 2, 64), (15, 0, 16, 1024), (16, 1, 16, 1024)]:
+        d = splitmix_bytes(seed, n)
+        a = oracle.split(table, d, bits=bits, min_size=mn)
+        b = oracle.py_split(table, d, bits=bits, min_size=mn)
+        assert [(int(x["offset"]), int(x["len"]), int(x["level"]), bytes(x["ref"])) for x in a] \
+            == [(y.offset, y.len, y.level, y.ref) for y in b]
+
+
+def test_multistream_oracle_equals_single(oracle, table):
+    from bs_amd.synth import splitmix_array
+    arrs = [splitmix_array(100 + i, n) for i, n in enumerate([0, 1, 5000, 70000, 200_000])]
+    base = np.concatenate(arrs)
+    lens = [len(a) for a in arrs]
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    ch, counts = oracle.split_streams(table, base, off, lens, bits=10, min_size=256, threads=3)
+    k = 0
+    for i, a in enumerate(arrs):
+        one = oracle.split(table, a, bits=10, min_size=256)
+        assert counts[i] == len(one)
+        got = ch[k:k + len(one)]
+        assert (got["offset"] == one["offset"]).all() and (got["ref"] == one["ref"]).all()
+        assert (got["stream"] == i).all()
+        k += len(one)
