@@ -46,16 +46,16 @@ def parse():
 
 
 def dist_setup():
-    import torch
+    """One process per GPU. Ranks only exchange a barrier and one float (max elapsed time), so
+    the process group is gloo over 127.0.0.1: the data path has no collective, and torch's own
+    (bundled) HIP runtime is never initialised next to libbsgpu's."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="gloo")
     return world, rank, local
 
 
@@ -70,8 +70,7 @@ def max_over_ranks(x: float, world: int) -> float:
         return x
     import torch
     import torch.distributed as dist
-    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -114,28 +113,26 @@ def cpu_baseline(sample_mib: int, bits: int, min_size: int) -> dict | None:
 def main():
     args = parse()
     world, rank, local = dist_setup()
-    import torch
     from bs_amd import build, bsgpu
 
     build.build()
-    assert torch.cuda.is_available(), "bench.py needs a GPU (the HIP path is the product)"
-    torch.cuda.set_device(local)
+    assert bsgpu.device_count() > local, "bench.py needs a GPU (the HIP path is the product)"
     nbytes = args.stream_mib << 20
     ns = args.streams
     stride = (nbytes + 15) & ~15
-    buf = torch.empty(stride * ns, dtype=torch.uint8, device=f"cuda:{local}")
+    buf = bsgpu.DeviceBuffer(stride * ns, device=local)
     eng = bsgpu.Engine(device=local)
     eng.profile(True)
     offs = [i * stride for i in range(ns)]
     lens = [nbytes] * ns
     for i in range(ns):  # stream s of rank r uses seed BASE + r*ns + s
-        bsgpu.fill_splitmix(buf.data_ptr() + offs[i], nbytes, BASE_SEED + rank * ns + i,
+        bsgpu.fill_splitmix(buf.ptr + offs[i], nbytes, BASE_SEED + rank * ns + i,
                             stream=eng.stream, device=local)
     stage_sum = [0.0, 0.0, 0.0]
     nsteps = [0]
 
     def step():
-        eng.run(buf.data_ptr(), offs, lens, bits=args.bits, min_size=args.min_size)
+        eng.run(buf.ptr, offs, lens, bits=args.bits, min_size=args.min_size)
         eng.finish()  # waits on the engine's stream; records stay in HBM
         ms = eng.stage_ms()
         for i in range(3):
@@ -143,7 +140,7 @@ def main():
         nsteps[0] += 1
 
     def sync():
-        torch.cuda.synchronize(local)
+        bsgpu.synchronize(local)
 
     # warmup steps are counted into stage_sum too; reset after them
     for _ in range(args.warmup):

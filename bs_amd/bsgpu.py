@@ -90,6 +90,10 @@ def lib() -> ctypes.CDLL:
         "bsg_sha256_batch": (ctypes.c_int, [ctypes.c_int, vp, u64p, u64p, ctypes.c_uint32, vp]),
         "bsg_fill_splitmix": (ctypes.c_int, [ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64,
                                              vp]),
+        "bsg_device_malloc": (vp, [ctypes.c_int, ctypes.c_size_t]),
+        "bsg_device_free": (ctypes.c_int, [ctypes.c_int, vp]),
+        "bsg_memcpy": (ctypes.c_int, [ctypes.c_int, vp, vp, ctypes.c_size_t, ctypes.c_int]),
+        "bsg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -176,6 +180,44 @@ def sha256_batch(blobs: list[bytes], device: int = 0) -> list[bytes]:
 def fill_splitmix(ptr: int, nbytes: int, seed: int, stream: int | None = None,
                   device: int = 0) -> None:
     _check(lib().bsg_fill_splitmix(device, ptr, nbytes, seed, stream), "bsg_fill_splitmix")
+
+
+class DeviceBuffer:
+    """Raw HIP allocation owned by libbsgpu (torch ships its own HIP runtime, so GPU processes
+    here never initialise torch's CUDA/HIP side)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device, self.nbytes = device, nbytes
+        self.ptr = lib().bsg_device_malloc(device, nbytes)
+        if not self.ptr:
+            raise BsgError(-12, "bsg_device_malloc")
+
+    def to_host(self, offset: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.nbytes - offset if n is None else n
+        out = np.empty(max(n, 1), dtype=np.uint8)
+        _check(lib().bsg_memcpy(self.device, out.ctypes.data, self.ptr + offset, n, 1),
+               "bsg_memcpy")
+        return out[:n]
+
+    def from_host(self, a: np.ndarray, offset: int = 0) -> None:
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        _check(lib().bsg_memcpy(self.device, self.ptr + offset, a.ctypes.data, a.nbytes, 0),
+               "bsg_memcpy")
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().bsg_device_free(self.device, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def synchronize(device: int = 0) -> None:
+    _check(lib().bsg_device_synchronize(device), "bsg_device_synchronize")
 
 
 class Engine:

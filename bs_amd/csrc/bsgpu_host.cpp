@@ -645,6 +645,40 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
   return rc;
 }
 
+void* bsg_device_malloc(int device, size_t bytes) {
+  if (device < 0 || device >= bsg_device_count() || hipSetDevice(device) != hipSuccess)
+    return nullptr;
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+int bsg_device_free(int device, void* p) {
+  if (!p) return BSG_OK;
+  HCHECK(hipSetDevice(device));
+  HCHECK(hipFree(p));
+  return BSG_OK;
+}
+
+int bsg_memcpy(int device, void* dst, const void* src, size_t n, int kind) {
+  if (n && (!dst || !src)) return BSG_EINVAL;
+  HCHECK(hipSetDevice(device));
+  hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                  : kind == 1 ? hipMemcpyDeviceToHost
+                              : hipMemcpyDeviceToDevice;
+  if (n) HCHECK(hipMemcpy(dst, src, n, k));
+  return BSG_OK;
+}
+
+int bsg_device_synchronize(int device) {
+  HCHECK(hipSetDevice(device));
+  HCHECK(hipDeviceSynchronize());
+  return BSG_OK;
+}
+
 int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed, void* stream) {
   if (!d_ptr && nbytes) return BSG_EINVAL;
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;

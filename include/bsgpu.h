@@ -120,6 +120,13 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
 int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                      uint32_t n, uint8_t* refs);
 
+/* Device memory helpers (so callers need no second HIP runtime): kind 0 = H2D, 1 = D2H,
+ * 2 = D2D. */
+void* bsg_device_malloc(int device, size_t bytes);
+int bsg_device_free(int device, void* p);
+int bsg_memcpy(int device, void* dst, const void* src, size_t n, int kind);
+int bsg_device_synchronize(int device);
+
 /* Utility (benchmarks/tests, not part of the reference surface): fill device memory with the
  * SplitMix64 counter stream of bs_amd/synth.py (word i = splitmix64(seed + (i+1)*0x9E37...)). */
 int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed, void* stream);

@@ -164,16 +164,15 @@ def test_streaming_small_and_empty(gpu, oracle, table):
 # Device-resident engine (the bench path) at full size
 # --------------------------------------------------------------------------------------------
 def _device_stream_run(gpu, nbytes_list, seed0, bits=16, min_size=1024):
-    import torch
     offs, total = [], 0
     for n in nbytes_list:
         offs.append(total)
         total += (n + 15) & ~15
-    buf = torch.empty(max(total, 16), dtype=torch.uint8, device="cuda")
+    buf = gpu.DeviceBuffer(max(total, 16))
     eng = gpu.Engine()
     for i, (o, n) in enumerate(zip(offs, nbytes_list)):
-        gpu.fill_splitmix(buf.data_ptr() + o, n, seed0 + i, stream=eng.stream)
-    eng.run(buf.data_ptr(), offs, nbytes_list, bits=bits, min_size=min_size)
+        gpu.fill_splitmix(buf.ptr + o, n, seed0 + i, stream=eng.stream)
+    eng.run(buf.ptr, offs, nbytes_list, bits=bits, min_size=min_size)
     eng.finish()
     return eng, buf, offs
 
@@ -187,7 +186,7 @@ def test_engine_device_resident_vs_oracle(gpu, oracle, table):
     k = 0
     for i, n in enumerate(lens):
         host = splitmix_array(0xB5B52026 + i, n)
-        dev = buf[offs[i]:offs[i] + n].cpu().numpy()
+        dev = buf.to_host(offs[i], n)
         assert np.array_equal(host, dev)  # device generator == host generator
         one = oracle.split(table, host)
         assert as_tuples(ch[k:k + int(counts[i])]) == as_tuples(one)
