@@ -193,6 +193,7 @@ def main():
             "cpu_baseline": cpu,
             "stage_ms": {n: round(v, 4) for n, v in zip(names, stage_avg)},
             "chunks_per_step": int(chunks),
+            "sha_path": eng.diag(),
         }
         if check is not None:
             line["oracle_check"] = check

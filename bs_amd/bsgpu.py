@@ -16,7 +16,7 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbsgpu.so")
+LIB_PATH = os.environ.get("BSG_LIB_PATH") or os.path.join(_HERE, "libbsgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bsgpu.h")
 
 BSG_OK = 0
@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
         "bsg_engine_stream": (vp, [vp]),
         "bsg_engine_candidates": (ctypes.c_uint64, [vp]),
         "bsg_engine_profile": (ctypes.c_int, [vp, ctypes.c_int]),
+        "bsg_engine_diag": (ctypes.c_int, [vp, u64p]),
         "bsg_engine_stage_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
         "bsg_split_hash_batch": (ctypes.c_int, [ctypes.c_int, vp, u64p, u64p, ctypes.c_uint32,
                                                 ctypes.POINTER(Params), u32p, vp,
@@ -268,6 +269,19 @@ class Engine:
         out = (ctypes.c_float * 3)()
         _check(lib().bsg_engine_stage_ms(self.h, out), "bsg_engine_stage_ms")
         return [float(x) for x in out]
+
+    def diag(self) -> dict:
+        d = np.zeros(16, dtype=np.uint64)
+        _check(lib().bsg_engine_diag(self.h, _p(d, ctypes.c_uint64)), "bsg_engine_diag")
+        out = {"nlong": int(d[0]), "long_thresh": int(d[1]), "max_nblocks": int(d[2]),
+               "nshort": int(d[13])}
+        for tag, o in (("long", 3), ("lane", 8)):
+            cyc, rt, nb = int(d[o + 1] - d[o]), int(d[o + 3] - d[o + 2]), int(d[o + 4])
+            if nb and rt:
+                out[tag] = {"blocks": nb, "cycles_per_block": round(cyc / nb, 1),
+                            "clock_ghz": round(cyc / (rt * 10.0), 3),
+                            "us_per_block": round(rt * 0.01 / nb, 4)}
+        return out
 
     @property
     def candidates(self) -> int:

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbsgpu.so")
 SOURCES = ["bsgpu_kernels.hip", "bsgpu_host.cpp"]
-HEADERS = ["bsgpu_internal.h", "bsgpu_launch.h", "buzhash32_table.inc"]
+HEADERS = ["bsgpu_internal.h", "bsgpu_launch.h", "buzhash32_table.inc", "sha256_device.h"]
 ARCH = os.environ.get("BSG_OFFLOAD_ARCH", "gfx950")
 
 
@@ -20,6 +20,17 @@ def _stale() -> bool:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(os.path.dirname(HERE), "include", "bsgpu.h"))
     return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_debug(extra=(), name="libbsgpu_dbg.so") -> str:
+    """Device-printf build (libbsgpu_dbg.so) for chasing hangs; never loaded by default."""
+    out = os.path.join(HERE, name)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-value", "-Wno-unused-result", *extra, "-o", out]
+    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    subprocess.run(cmd, check=True)
+    return out
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

@@ -81,6 +81,33 @@ struct PinBuf {
 
 int herr(hipError_t e) { return e == hipSuccess ? BSG_OK : BSG_EDEVICE; }
 
+// BSG_DEBUG_SYNC=1: synchronise and report after every launch (debugging hangs/faults)
+bool debug_sync() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("BSG_DEBUG_SYNC");
+    v = (e && *e == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+hipError_t dbg(const char* what, hipStream_t s, hipError_t e) {
+  if (!debug_sync() || e != hipSuccess) return e;
+  std::fprintf(stderr, "bsgpu: %s ...", what);
+  std::fflush(stderr);
+  e = hipStreamSynchronize(s);
+  std::fprintf(stderr, " %s\n", hipGetErrorString(e));
+  std::fflush(stderr);
+  return e;
+}
+
+int long_mode() {  // BSG_LONG_MODE = off | all (experiments); default auto
+  const char* e = std::getenv("BSG_LONG_MODE");
+  if (!e) return 0;
+  if (!std::strcmp(e, "off")) return 1;
+  if (!std::strcmp(e, "all")) return 2;
+  return 0;
+}
+
 #define HCHECK(x)                           \
   do {                                      \
     hipError_t e_ = (x);                    \
@@ -111,7 +138,7 @@ struct bsg_engine {
   int num_cus = 256;
   hipStream_t stream = nullptr;
   DevBuf table, streams, strip0, counts, slots, strip_off, partials_a, partials_b, cand, flags,
-      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr;
+      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets;
   PinBuf h_streams, h_strip0, h_ctr;
   // current run
   const uint8_t* d_data = nullptr;
@@ -172,6 +199,9 @@ struct bsg_engine {
     HCHECK(last_end.ensure(sizeof(uint64_t) * (ns ? ns : 1)));
     HCHECK(carry.ensure(sizeof(CarryOut) * (ns ? ns : 1)));
     HCHECK(ctr.ensure(sizeof(Counters)));
+    HCHECK(long_list.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
+    HCHECK(order.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
+    HCHECK(buckets.ensure(sizeof(uint32_t) * 2 * kLptBuckets));
     HCHECK(h_streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(h_strip0.ensure(sizeof(uint64_t) * (ns + 1)));
     HCHECK(h_ctr.ensure(sizeof(Counters)));
@@ -184,11 +214,12 @@ struct bsg_engine {
     HCHECK(hipMemcpyAsync(strip0.p, h_strip0.p, sizeof(uint64_t) * (ns + 1),
                           hipMemcpyHostToDevice, stream));
     HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
+    HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * kLptBuckets, stream));
     Counters* dctr = ctr.as<Counters>();
 
     InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
                 carry.as<CarryOut>()};
-    if (ns) HCHECK(launch_init(ia, stream));
+    if (ns) HCHECK(dbg("launch_init", stream, launch_init(ia, stream)));
 
     ScanArgs sa{};
     sa.data = d_data;
@@ -205,7 +236,7 @@ struct bsg_engine {
     sa.cand_cap = cand_cap;
     sa.ctr = dctr;
     mark(0);
-    if (strips) HCHECK(launch_scan(sa, stream, num_cus));
+    if (strips) HCHECK(dbg("launch_scan", stream, launch_scan(sa, stream, num_cus)));
     mark(1);
 
     PrefixArgs pa{};
@@ -218,12 +249,12 @@ struct bsg_engine {
     pa.overflow = &dctr->overflow;
     pa.cap = cand_cap;
     pa.skip_if = nullptr;
-    HCHECK(launch_prefix(pa, stream));
+    HCHECK(dbg("launch_prefix", stream, launch_prefix(pa, stream)));
 
-    if (strips) HCHECK(launch_compact(sa, stream, num_cus));
+    if (strips) HCHECK(dbg("launch_compact", stream, launch_compact(sa, stream, num_cus)));
 
     SelArgs sel{cand.as<uint64_t>(), streams.as<StreamDesc>(), flags.as<uint32_t>(), p, dctr};
-    HCHECK(launch_select(sel, cand_cap, stream, num_cus));
+    HCHECK(dbg("launch_select", stream, launch_select(sel, cand_cap, stream, num_cus)));
 
     PrefixArgs pf{};
     pf.in = flags.as<uint32_t>();
@@ -235,18 +266,20 @@ struct bsg_engine {
     pf.overflow = nullptr;
     pf.cap = 0;
     pf.skip_if = &dctr->overflow;
-    HCHECK(launch_prefix(pf, stream));
+    HCHECK(dbg("launch_prefix", stream, launch_prefix(pf, stream)));
 
     ChunkArgs ca{cand.as<uint64_t>(), flags.as<uint32_t>(), fidx.as<uint64_t>(),
                  bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
                  last_end.as<uint64_t>(), chunk_cap, p, dctr};
-    HCHECK(launch_chunks(ca, cand_cap, stream, num_cus));
+    HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, stream, num_cus)));
 
     ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
                bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
-               carry.as<CarryOut>(), chunk_cap};
+               carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
+               buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets, long_mode()};
+    HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
-    HCHECK(launch_sha(sh, chunk_cap + ns, stream, num_cus));
+    HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
     mark(3);
     enqueued = true;
     return BSG_OK;
@@ -431,7 +464,7 @@ void bsg_engine_destroy(bsg_engine* e) {
   DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->slots,
                     &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
                     &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
-                    &e->out, &e->carry, &e->ctr};
+                    &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 4; ++i)
     if (e->ev[i]) hipEventDestroy(e->ev[i]);
@@ -516,6 +549,18 @@ int bsg_engine_stage_ms(const bsg_engine* e, float out[3]) {
 }
 
 uint64_t bsg_engine_candidates(const bsg_engine* e) { return e ? e->last.ncand : 0; }
+
+int bsg_engine_diag(const bsg_engine* e, uint64_t out[16]) {
+  if (!e || !out) return BSG_EINVAL;
+  out[0] = e->last.nlong;
+  out[1] = e->last.long_thresh;
+  out[2] = e->last.max_nblocks;
+  for (int i = 0; i < 5; ++i) out[3 + i] = e->last.diag[i];
+  for (int i = 0; i < 5; ++i) out[8 + i] = e->last.diag2[i];
+  out[13] = e->last.nshort;
+  out[14] = out[15] = 0;
+  return BSG_OK;
+}
 
 bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, int* err) {
   int dummy;

@@ -84,7 +84,20 @@ struct Counters {
   uint64_t job_head;           // SHA-256 dynamic work queue head
   uint64_t overflow;           // candidate buffer too small (host grows and re-runs)
   uint64_t error;              // device-side sanity check failed (bug guard; run is invalid)
-  uint64_t pad_[3];
+  uint64_t max_nblocks;        // longest SHA-256 job in blocks (k_lens)
+  uint64_t long_thresh;        // jobs with >= this many blocks run on the wave-per-chunk path
+  uint64_t nlong;              // number of such jobs (k_longlist)
+  uint64_t long_head;          // k_sha_long work queue head
+  uint64_t nshort;             // jobs on the per-lane path (k_bucket_scatter)
+  uint64_t bucket_width;       // LPT bucket width in blocks
+  uint64_t diag[5];            // k_sha_long job 0: memtime0/1, realtime0/1, nblocks (diagnostic)
+  uint64_t diag2[5];           // k_sha per-lane job order[0]: same fields
+  uint64_t pad_[11];
 };
+static_assert(sizeof(Counters) == 256, "Counters layout");
+
+constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave-per-chunk path below 64 KiB
+constexpr int kLongRow = 68;               // LDS words per K+W row (64 + pad: conflict-free b128)
+constexpr int kLptBuckets = 4096;          // longest-first job order: counting sort on nblocks
 
 }  // namespace bsg

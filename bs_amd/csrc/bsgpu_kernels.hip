@@ -18,22 +18,13 @@
 
 #include "bsgpu_internal.h"
 #include "bsgpu_launch.h"
+#include "sha256_device.h"
 
 namespace bsg {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(16)));
 
-__device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
-__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t r) {
-  return __builtin_amdgcn_alignbit(x, x, r);
-}
-// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
 __device__ __forceinline__ uint32_t tz32(uint32_t h) { return h ? (uint32_t)__builtin_ctz(h) : 32u; }
 
 __device__ __forceinline__ void load16(const uint8_t* p, uint32_t (&w)[16]) {
@@ -409,49 +400,6 @@ __global__ void k_init(InitArgs a) {
 // jobs from a device queue as they finish, so a wave stays full whatever the length mix.
 // Jobs [0, M) are finished chunks; jobs [M, M + nstreams) are the open chunks of non-final
 // segments (hash whole blocks only, export the midstate).
-// ---------------------------------------------------------------------------------------------
-__constant__ uint32_t kK256[64] = {
-    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
-    0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
-    0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
-    0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
-    0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
-    0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
-    0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
-    0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
-    0xc67178f2};
-
-__device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&W)[16]) {
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
-           h = st[7];
-#pragma unroll
-  for (int t = 0; t < 64; ++t) {
-    if (t >= 16) {
-      const uint32_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
-      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-      W[t & 15] += s0 + W[(t - 7) & 15] + s1;
-    }
-    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-    const uint32_t ch = (e & f) | (~e & g);
-    const uint32_t t1 = h + S1 + ch + kK256[t] + W[t & 15];
-    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-    const uint32_t ab = a ^ b;
-    const uint32_t mj = (ab & c) | (~ab & b);
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + S0 + mj;
-  }
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
-}
-
 struct ShaJob {
   uint64_t id;          // job index
   uint64_t start, end;  // stream offsets [start, end)
@@ -465,6 +413,10 @@ struct ShaJob {
   uint32_t level;
   uint32_t stream;
 };
+
+__device__ __forceinline__ bool is_long(const ShaJob& jb, uint64_t thresh) {
+  return jb.prefix == 0 && jb.nblocks >= thresh;
+}
 
 __device__ bool sha_setup(const ShaArgs& a, uint64_t j, uint64_t M, ShaJob& jb,
                           uint32_t (&st)[8]) {
@@ -515,22 +467,60 @@ __device__ bool sha_setup(const ShaArgs& a, uint64_t j, uint64_t M, ShaJob& jb,
   return true;
 }
 
-__device__ __forceinline__ void sha_load_fast(const uint8_t* p, uint32_t (&W)[16]) {
-  // 16 big-endian words from an arbitrary byte address: aligned dword loads + v_perm_b32
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
-  const uint32_t sh = (uint32_t)(addr & 3u);
-  const uint32_t* al = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+// Raw (unaligned) 64-byte block: 17 aligned dwords + a v_perm_b32 selector that both realigns
+// and byte-swaps, plus the number of valid message bytes in the block (<64 only at a chunk's
+// end). Issued one block ahead so the load latency hides under the compression.
+struct RawBlock {
   uint32_t r[17];
-  const u32x4* q = reinterpret_cast<const u32x4*>(al);
+  uint32_t sel;
+  int32_t valid;  // message bytes of this block that are data: 64 (full), 0..63 (tail), -1 (pad)
+};
+
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+
+// Block at message offset o0 (>= prefix) of a job whose data bytes are dbase[o - prefix].
+// Branch-free on purpose: the same 17 dword loads into the same registers every time, so the
+// compiler never has to drain a prefetch at a control-flow join. Every load is in bounds: a
+// dword holding at least one valid byte never crosses a page, dwords past the valid range are
+// clamped onto the last one holding a valid byte, and a block with no data bytes reads the
+// always-valid `safe` address instead (its bytes are masked off by pad_words).
+__device__ __forceinline__ void raw_load(const uint8_t* dbase, uint64_t o0, uint32_t prefix,
+                                         uint64_t L, const void* safe, RawBlock& rb) {
+  const uint8_t* p = dbase + (o0 - prefix);
+  const int64_t vv = (int64_t)L - (int64_t)o0;
+  const int32_t v = vv < 0 ? -1 : (vv >= 64 ? 64 : (int32_t)vv);
+  const uintptr_t addr = v > 0 ? reinterpret_cast<uintptr_t>(p)
+                               : reinterpret_cast<uintptr_t>(safe) & ~(uintptr_t)3;
+  const uint32_t sh = (uint32_t)(addr & 3u);
+  gu32* al = reinterpret_cast<gu32*>(addr & ~(uintptr_t)3);
+  const uint32_t jmax = v > 0 ? ((uint32_t)v + sh - 1) >> 2 : 0u;
+  rb.sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
+  rb.valid = v;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    u32x4 v = q[i];
-    r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+  for (int j = 0; j < 17; ++j) rb.r[j] = al[min((uint32_t)j, jmax)];
+}
+
+__device__ __forceinline__ void raw_to_words(const RawBlock& rb, uint32_t (&W)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(rb.r[i + 1], rb.r[i], rb.sel);
+}
+
+// Tail block: keep the valid bytes, append 0x80, zero the rest (FIPS 180-4 §5.1.1).
+__device__ __forceinline__ void pad_words(int32_t valid, uint32_t (&W)[16]) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int32_t k = valid - 4 * q;  // valid bytes in word q
+    const uint32_t keep = k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : (0xffffffffu << (32 - 8 * k)));
+    const uint32_t pad = (k >= 0 && k < 4) ? (0x80u << (24 - 8 * k)) : 0u;
+    W[q] = (W[q] & keep) | pad;
   }
-  r[16] = sh ? al[16] : 0u;  // an aligned dword holding a needed byte never crosses a page
-  const uint32_t sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(r[i + 1], r[i], sel);
+}
+
+__device__ __forceinline__ void sha_load_fast(const uint8_t* p, uint32_t (&W)[16]) {
+  RawBlock rb;
+  raw_load(p, 0, 0, 64, p, rb);
+  raw_to_words(rb, W);
 }
 
 __device__ __forceinline__ void sha_load_slow(const ShaJob& jb, uint32_t blk, uint32_t (&W)[16]) {
@@ -577,37 +567,286 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
   }
 }
 
-__global__ __launch_bounds__(256) void k_sha(ShaArgs a) {
-  if (a.ctr->overflow || a.ctr->error) return;
-  const uint64_t M = a.ctr->nchunks;
-  if (M > a.chunk_cap) return;  // k_chunks flagged the error
-  const uint64_t njobs = M + a.nstreams;
+// Per-lane mode: each lane hashes one chunk at a time, pulling jobs from the longest-first
+// order as it finishes (dynamic per-lane queue).
+__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
+  const uint64_t nshort = a.ctr->nshort;
   ShaJob jb;
   uint32_t st[8];
+  RawBlock rb;
   bool has = false, exhausted = false;
   uint32_t blk = 0;
+  uint64_t tm0 = 0, tr0 = 0;
+  bool stamp = false;
   for (;;) {
     while (!has && !exhausted) {
-      const uint64_t j = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->job_head), 1ull);
-      if (j >= njobs) {
+      const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->job_head), 1ull);
+      if (q >= nshort) {
         exhausted = true;
-      } else if (sha_setup(a, j, M, jb, st)) {
+      } else if (sha_setup(a, a.order[q], M, jb, st)) {
+        stamp = (q == 0);  // diagnostic timing of the longest per-lane job
+        if (stamp) {
+          tm0 = __builtin_amdgcn_s_memtime();
+          tr0 = __builtin_amdgcn_s_memrealtime();
+        }
         blk = 0;
-        if (jb.nblocks == 0) sha_finish(a, jb, st);
-        else has = true;
+        if (jb.nblocks == 0) {
+          sha_finish(a, jb, st);
+        } else {
+          has = true;
+          if (jb.prefix == 0) raw_load(jb.dbase, 0, 0, jb.L, a.streams, rb);
+        }
       }
     }
     if (!has) break;
     uint32_t W[16];
     const uint64_t o0 = 64ull * blk;
-    if (o0 >= jb.prefix && o0 + 64 <= jb.L) sha_load_fast(jb.dbase + (o0 - jb.prefix), W);
-    else sha_load_slow(jb, blk, W);
+    if (o0 >= jb.prefix) {
+      raw_to_words(rb, W);
+      if (rb.valid < 64) {
+        pad_words(rb.valid, W);
+        if (jb.fin && blk + 1 == jb.nblocks) {
+          const uint64_t bits = (jb.consumed + jb.L) * 8ull;
+          W[14] = (uint32_t)(bits >> 32);
+          W[15] = (uint32_t)bits;
+        }
+      }
+    } else {
+      sha_load_slow(jb, blk, W);  // head block of a continued chunk (once per segment)
+    }
+    // prefetch the next block, unconditionally (past the last block it reads the safe
+    // address): a branch here would make the compiler drain vmcnt at the join
+    raw_load(jb.dbase, o0 + 64, jb.prefix, jb.L, a.streams, rb);
     sha256_compress(st, W);
     if (++blk == jb.nblocks) {
       sha_finish(a, jb, st);
       has = false;
+      if (stamp) {
+        a.ctr->diag2[1] = __builtin_amdgcn_s_memtime();
+        a.ctr->diag2[3] = __builtin_amdgcn_s_memrealtime();
+        a.ctr->diag2[0] = tm0;
+        a.ctr->diag2[2] = tr0;
+        a.ctr->diag2[4] = jb.nblocks;
+        stamp = false;
+      }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-per-chunk path for the longest chunks. A SHA-256 chain is serial, so a batch's wall time
+// is its longest chunk's chain; a lone lane of a mostly finished wave issues at ~5.2 cycles per
+// VALU op, a full wave at ~4.1. Here one 64-lane wave owns one long chunk: all lanes build the
+// message schedule (K+W) of 64 consecutive blocks at once into an LDS ring, then the wave runs
+// the 64 rounds of each block uniformly (~14 VALU per round) reading K+W by broadcast
+// ds_read_b128. Jobs with >= long_thresh blocks (max(1024, longest/2)) take this path.
+// ---------------------------------------------------------------------------------------------
+// Job ordering: long jobs -> long_list; the rest counting-sorted on nblocks, longest first
+// (LPT), so the lanes of one wave hold chunks of similar length and finish together.
+__device__ __forceinline__ uint32_t lpt_bucket(const Counters* ctr, uint32_t nblocks) {
+  const uint64_t mx = ctr->max_nblocks;
+  const uint64_t d = mx > nblocks ? mx - nblocks : 0;
+  const uint64_t b = d / ctr->bucket_width;
+  return b < (uint64_t)kLptBuckets ? (uint32_t)b : (uint32_t)(kLptBuckets - 1);
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_order(ShaArgs a) {
+  if (a.ctr->overflow || a.ctr->error) return;
+  const uint64_t M = a.ctr->nchunks;
+  if (M > a.chunk_cap) return;
+  const uint64_t njobs = M + a.nstreams;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t thresh = a.ctr->long_thresh;
+  uint32_t st[8];
+  ShaJob jb;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < njobs; j += stride) {
+    if (!sha_setup(a, j, M, jb, st)) continue;
+    if (is_long(jb, thresh)) {
+      if (SCATTER) {
+        const uint64_t k = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->nlong), 1ull);
+        a.long_list[k] = j;
+      }
+      continue;
+    }
+    const uint32_t b = lpt_bucket(a.ctr, jb.nblocks);
+    if (!SCATTER) {
+      atomicAdd(a.bucket_cnt + b, 1u);
+    } else {
+      const uint32_t pos = atomicAdd(a.bucket_off + b, 1u);
+      a.order[pos] = j;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
+  // exclusive scan of kLptBuckets counts (4 per thread) -> bucket_off; total -> nshort
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[i] = a.bucket_cnt[4 * t + i]; sum += v[i]; }
+  uint32_t x = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((t & 63) >= (uint32_t)o) x += y;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) pre += wsum[w];
+  pre += x - sum;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { a.bucket_off[4 * t + i] = pre; pre += v[i]; }
+  if (t == 1023) a.ctr->nshort = pre;
+}
+
+__global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
+  if (a.ctr->overflow || a.ctr->error) return;
+  const uint64_t M = a.ctr->nchunks;
+  if (M > a.chunk_cap) return;
+  const uint64_t njobs = M + a.nstreams;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t st[8];
+  ShaJob jb;
+  uint64_t mx = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < njobs; j += stride)
+    if (sha_setup(a, j, M, jb, st) && jb.prefix == 0) mx = max(mx, (uint64_t)jb.nblocks);
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint64_t)__shfl_down(mx, o));
+  if ((threadIdx.x & 63) == 0 && mx)
+    atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->max_nblocks), (unsigned long long)mx);
+}
+
+__global__ void k_thresh(Counters* ctr, int mode) {
+  // Wave-per-chunk path for jobs >= 60% of the longest: a per-lane wave runs ~1480 VALU per
+  // block against the wave path's ~930, so both paths' longest jobs then end together.
+  const uint64_t t = (ctr->max_nblocks * 3 + 4) / 5;
+  ctr->long_thresh = t > kLongMinBlocks ? t : (uint64_t)kLongMinBlocks;
+  const uint64_t w = (ctr->max_nblocks + kLptBuckets) / kLptBuckets;
+  ctr->bucket_width = w ? w : 1;
+  if (mode == 1) ctr->long_thresh = ~0ull;  // BSG_LONG_MODE=off: per-lane only
+  if (mode == 2) ctr->long_thresh = 0;      // BSG_LONG_MODE=all: wave mode for everything
+}
+
+// Orders one wave's LDS ring writes before its reads (and reads before the next writes). The
+// ring is private to the wave, and a wave's LDS operations are executed in order, so only the
+// compiler has to be kept from reordering: a wave-scope fence, no s_barrier (the other waves
+// of the workgroup run independent jobs).
+__device__ __forceinline__ void ring_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Wave mode: the whole wave hashes long job j; ring = this wave's 64 x kLongRow LDS words.
+__device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t j,
+                             uint32_t* ring) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ShaJob jb;
+  uint32_t st[8];
+  sha_setup(a, j, M, jb, st);
+  uint64_t tm0 = 0, tr0 = 0;
+  if (li == 0) {  // timing stamps of one job (read back as Counters::diag)
+    tm0 = __builtin_amdgcn_s_memtime();
+    tr0 = __builtin_amdgcn_s_memrealtime();
+  }
+  const uint32_t nblocks = __builtin_amdgcn_readfirstlane(jb.nblocks);
+  for (uint32_t base = 0; base < nblocks; base += 64) {
+    // phase A: lane i expands block base+i into K+W (LDS row i)
+    const uint32_t blk = base + lane;
+    RawBlock rb;
+    raw_load(jb.dbase, 64ull * blk, 0, jb.L, a.streams, rb);
+    uint32_t W[16];
+    raw_to_words(rb, W);
+    if (rb.valid < 64) {
+      pad_words(rb.valid, W);
+      if (jb.fin && blk + 1 == jb.nblocks) {
+        const uint64_t bits = (jb.consumed + jb.L) * 8ull;
+        W[14] = (uint32_t)(bits >> 32);
+        W[15] = (uint32_t)bits;
+      }
+    }
+    u32x4a* row = reinterpret_cast<u32x4a*>(ring + lane * kLongRow);
+#pragma unroll
+    for (int t = 0; t < 64; t += 4) {
+      uint32_t kw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = t + u;
+        if (i >= 16) {
+          const uint32_t w15 = W[(i - 15) & 15], w2 = W[(i - 2) & 15];
+          const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+          const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+          W[i & 15] = (W[i & 15] + s0) + (W[(i - 7) & 15] + s1);
+        }
+        kw[u] = kK256[i] + W[i & 15];
+      }
+      row[t / 4] = u32x4a{kw[0], kw[1], kw[2], kw[3]};
+    }
+    ring_sync();
+    // phase B: the wave runs the rounds of blocks base .. base+63 uniformly
+    const uint32_t nb = min(64u, nblocks - base);
+    for (uint32_t i = 0; i < nb; ++i) {
+      const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + i * kLongRow);
+      uint32_t KW[64];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const u32x4a v = r[q];
+        KW[4 * q] = v.x; KW[4 * q + 1] = v.y; KW[4 * q + 2] = v.z; KW[4 * q + 3] = v.w;
+      }
+      sha256_rounds_kw<true>(st, KW);
+    }
+    ring_sync();
+  }
+  if (lane == 0) {
+    sha_finish(a, jb, st);
+    if (li == 0) {
+      a.ctr->diag[1] = __builtin_amdgcn_s_memtime();
+      a.ctr->diag[3] = __builtin_amdgcn_s_memrealtime();
+      a.ctr->diag[0] = tm0;
+      a.ctr->diag[2] = tr0;
+      a.ctr->diag[4] = jb.nblocks;
+    }
+  }
+}
+
+// The SHA-256 kernel. One 256-thread workgroup per CU (the LDS request admits only one), so
+// each of its 4 waves owns a SIMD: one wave saturates a SIMD's integer VALU (~4.2 cycles per
+// wave-instruction; a second wave on the same SIMD only runs in the first one's gaps), so
+// nothing is gained by stacking waves and the latency-critical wave-mode chains must not
+// share. Every wave first drains the long-job queue in wave mode, then turns per-lane.
+// Wave-uniform queue pop: lane 0 takes the ticket, every lane gets it as an SGPR value.
+__device__ __forceinline__ uint64_t pop_uniform(uint64_t* head) {
+  uint32_t lo = 0, hi = 0;
+  if ((threadIdx.x & 63u) == 0) {
+    const uint64_t t = atomicAdd(reinterpret_cast<unsigned long long*>(head), 1ull);
+    lo = (uint32_t)t;
+    hi = (uint32_t)(t >> 32);
+  }
+  lo = __builtin_amdgcn_readlane(lo, 0);
+  hi = __builtin_amdgcn_readlane(hi, 0);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// The SHA-256 kernel. One 256-thread workgroup per CU (its LDS request admits only one), so
+// each of the 4 waves owns a SIMD: one wave saturates a SIMD's integer VALU (~4.2 cycles per
+// wave-instruction; a second wave on the SIMD only runs in the first one's gaps), so stacking
+// waves gains nothing and would stall the latency-critical wave-mode chains. Every wave first
+// drains the long-job queue in wave mode, then turns to per-lane mode (longest-first order).
+__global__ __launch_bounds__(256, 1) void k_sha(ShaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  if (a.ctr->overflow || a.ctr->error) return;
+  const uint64_t M = a.ctr->nchunks;
+  if (M > a.chunk_cap) return;  // k_chunks flagged the error
+  const uint64_t nlong = a.ctr->nlong;
+  uint32_t* ring = lds + (threadIdx.x >> 6) * (64 * kLongRow);
+  // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
+  // break; }` form was restructured by hipcc into a nested loop that re-entered job 0 forever.
+  uint64_t li = pop_uniform(&a.ctr->long_head);
+  while (li < nlong) {
+    sha_wave_job(a, M, li, a.long_list[li], ring);
+    li = pop_uniform(&a.ctr->long_head);
+  }
+  sha_lane_mode(a, M);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -629,11 +868,20 @@ __global__ __launch_bounds__(256) void k_sha_blobs(BlobShaArgs a) {
     jb.nblocks = (uint32_t)((jb.L + 8) / 64 + 1);
     uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                       0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    RawBlock rb;
+    raw_load(jb.dbase, 0, 0, jb.L, a.off, rb);
     for (uint32_t blk = 0; blk < jb.nblocks; ++blk) {
       uint32_t W[16];
-      const uint64_t o0 = 64ull * blk;
-      if (o0 + 64 <= jb.L) sha_load_fast(jb.dbase + o0, W);
-      else sha_load_slow(jb, blk, W);
+      raw_to_words(rb, W);
+      if (rb.valid < 64) {
+        pad_words(rb.valid, W);
+        if (blk + 1 == jb.nblocks) {
+          const uint64_t bits = jb.L * 8ull;
+          W[14] = (uint32_t)(bits >> 32);
+          W[15] = (uint32_t)bits;
+        }
+      }
+      raw_load(jb.dbase, 64ull * (blk + 1), 0, jb.L, a.off, rb);
       sha256_compress(st, W);
     }
     uint32_t* ref = reinterpret_cast<uint32_t*>(a.refs + 32 * i);
@@ -724,10 +972,22 @@ hipError_t launch_init(const InitArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+constexpr uint32_t kShaLds = 84 * 1024;  // > 80 KiB: one k_sha workgroup per CU (160 KiB LDS)
+static_assert(4 * 64 * kLongRow * 4 <= kShaLds, "wave rings fit");
+
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
-  // enough lanes for every job, capped at ~8 waves per SIMD; idle lanes exit at once
-  const uint32_t grid = grid_for(job_bound, 256, 8u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_sha, dim3(grid), dim3(256), 0, s, a);
+  (void)job_bound;  // persistent: one workgroup per CU, waves loop over the job queues
+  hipLaunchKernelGGL(k_sha, dim3((uint32_t)num_cus), dim3(256), kShaLds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
+  const uint32_t grid = grid_for(job_bound, 256, 4u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_lens, dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_thresh, dim3(1), dim3(1), 0, s, a.ctr, a.long_mode);
+  hipLaunchKernelGGL(k_order<false>, dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_order<true>, dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -75,6 +75,11 @@ struct ShaArgs {
   ChunkRec* out;
   CarryOut* carry;
   uint64_t chunk_cap;
+  uint64_t* long_list;      // [chunk_cap + nstreams] job ids for the wave-per-chunk path
+  uint64_t* order;          // [chunk_cap + nstreams] per-lane jobs, longest first
+  uint32_t* bucket_cnt;     // [kLptBuckets] zeroed per run
+  uint32_t* bucket_off;     // [kLptBuckets]
+  int long_mode;            // 0 auto, 1 per-lane only, 2 wave mode only (experiments)
 };
 
 struct BlobShaArgs {
@@ -93,6 +98,7 @@ hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, i
 hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);
 hipError_t launch_init(const InitArgs& a, hipStream_t s);
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
+hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus);
 hipError_t launch_fill_splitmix(uint8_t* p, uint64_t n, uint64_t seed, hipStream_t s,
                                 int num_cus);

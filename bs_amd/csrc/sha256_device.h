@@ -1,0 +1,155 @@
+// sha256_device.h — CDNA4 device primitives shared by the kernels and tools/ubench:
+// rotates (v_alignbit_b32), 3-input bitwise ops (v_bitop3_b32) and the SHA-256 compression
+// function (FIPS 180-4 §6.2.2) fully unrolled with variables rotated by renaming.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bsg {
+
+__device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t r) {
+  return __builtin_amdgcn_alignbit(x, x, r);
+}
+// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+static constexpr uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+    0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+    0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+    0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+    0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+    0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+    0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+    0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2};
+
+template <uint32_t TT>
+__device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+  // v_bitop3_b32: bit i of the result = TT[(a_i << 2) | (b_i << 1) | c_i]
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
+  return r;
+}
+
+// One SHA-256 round, 14 VALU ops: 3+1 (Sigma1), Ch (bitop3 0xCA), h+K+W, add3, d += T1,
+// 3+1 (Sigma0), Maj (bitop3 0xE8), add3. Variables rotate by renaming, not by moves.
+#define SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                 \
+  do {                                                                         \
+    const uint32_t s1_ = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));           \
+    const uint32_t ch_ = bitop3<0xCA>(e, f, g);                                \
+    const uint32_t t1_ = (h + (kw)) + s1_ + ch_;                               \
+    d += t1_;                                                                  \
+    const uint32_t s0_ = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));           \
+    const uint32_t mj_ = bitop3<0xE8>(a, b, c);                                \
+    h = t1_ + s0_ + mj_;                                                       \
+  } while (0)
+
+__device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&W)[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+#pragma unroll
+  for (int t = 0; t < 64; t += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = t + u;
+      if (i >= 16) {
+        const uint32_t w15 = W[(i - 15) & 15], w2 = W[(i - 2) & 15];
+        const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+        const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        W[i & 15] = (W[i & 15] + s0) + (W[(i - 7) & 15] + s1);
+      }
+    }
+    SHA_ROUND(a, b, c, d, e, f, g, h, kK256[t + 0] + W[(t + 0) & 15]);
+    SHA_ROUND(h, a, b, c, d, e, f, g, kK256[t + 1] + W[(t + 1) & 15]);
+    SHA_ROUND(g, h, a, b, c, d, e, f, kK256[t + 2] + W[(t + 2) & 15]);
+    SHA_ROUND(f, g, h, a, b, c, d, e, kK256[t + 3] + W[(t + 3) & 15]);
+    SHA_ROUND(e, f, g, h, a, b, c, d, kK256[t + 4] + W[(t + 4) & 15]);
+    SHA_ROUND(d, e, f, g, h, a, b, c, kK256[t + 5] + W[(t + 5) & 15]);
+    SHA_ROUND(c, d, e, f, g, h, a, b, kK256[t + 6] + W[(t + 6) & 15]);
+    SHA_ROUND(b, c, d, e, f, g, h, a, kK256[t + 7] + W[(t + 7) & 15]);
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+
+// Variant for experiments (tools/ubench): plain C operators, left to hipcc's selection.
+#define SHA_ROUND_C(a, b, c, d, e, f, g, h, kw)                               \
+  do {                                                                         \
+    const uint32_t s1_ = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);               \
+    const uint32_t ch_ = (e & f) | (~e & g);                                   \
+    const uint32_t t1_ = (h + (kw)) + s1_ + ch_;                               \
+    d += t1_;                                                                  \
+    const uint32_t s0_ = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);               \
+    const uint32_t mj_ = (a & b) | (c & (a | b));                              \
+    h = t1_ + s0_ + mj_;                                                       \
+  } while (0)
+
+template <bool ASM>
+__device__ __forceinline__ void sha256_compress_v(uint32_t (&st)[8], uint32_t (&W)[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+#pragma unroll
+  for (int t = 0; t < 64; t += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = t + u;
+      if (i >= 16) {
+        const uint32_t w15 = W[(i - 15) & 15], w2 = W[(i - 2) & 15];
+        uint32_t s0, s1;
+        if (ASM) {
+          s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+          s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+        } else {
+          s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+          s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+        }
+        W[i & 15] = (W[i & 15] + s0) + (W[(i - 7) & 15] + s1);
+      }
+    }
+#define R_(...) do { if (ASM) SHA_ROUND(__VA_ARGS__); else SHA_ROUND_C(__VA_ARGS__); } while (0)
+    R_(a, b, c, d, e, f, g, h, kK256[t + 0] + W[(t + 0) & 15]);
+    R_(h, a, b, c, d, e, f, g, kK256[t + 1] + W[(t + 1) & 15]);
+    R_(g, h, a, b, c, d, e, f, kK256[t + 2] + W[(t + 2) & 15]);
+    R_(f, g, h, a, b, c, d, e, kK256[t + 3] + W[(t + 3) & 15]);
+    R_(e, f, g, h, a, b, c, d, kK256[t + 4] + W[(t + 4) & 15]);
+    R_(d, e, f, g, h, a, b, c, kK256[t + 5] + W[(t + 5) & 15]);
+    R_(c, d, e, f, g, h, a, b, kK256[t + 6] + W[(t + 6) & 15]);
+    R_(b, c, d, e, f, g, h, a, kK256[t + 7] + W[(t + 7) & 15]);
+#undef R_
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Rounds only, with K[t] + W[t] precomputed elsewhere (long-chain path experiments).
+template <bool ASM>
+__device__ __forceinline__ void sha256_rounds_kw(uint32_t (&st)[8], const uint32_t (&KW)[64]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+           h = st[7];
+#pragma unroll
+  for (int t = 0; t < 64; t += 8) {
+#define R_(...) do { if (ASM) SHA_ROUND(__VA_ARGS__); else SHA_ROUND_C(__VA_ARGS__); } while (0)
+    R_(a, b, c, d, e, f, g, h, KW[t + 0]);
+    R_(h, a, b, c, d, e, f, g, KW[t + 1]);
+    R_(g, h, a, b, c, d, e, f, KW[t + 2]);
+    R_(f, g, h, a, b, c, d, e, KW[t + 3]);
+    R_(e, f, g, h, a, b, c, d, KW[t + 4]);
+    R_(d, e, f, g, h, a, b, c, KW[t + 5]);
+    R_(c, d, e, f, g, h, a, b, KW[t + 6]);
+    R_(b, c, d, e, f, g, h, a, KW[t + 7]);
+#undef R_
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+}  // namespace bsg

@@ -106,6 +106,11 @@ void* bsg_engine_stream(bsg_engine* eng);
  * (k_sha). Timed on the engine's own stream. */
 int bsg_engine_profile(bsg_engine* eng, int enable);
 int bsg_engine_stage_ms(const bsg_engine* eng, float out[3]);
+/* Diagnostics of the last run: [0] jobs on the wave-per-chunk path, [1] its block threshold,
+ * [2] longest job (blocks), [3..7] one long job's s_memtime start/end, s_memrealtime
+ * start/end (100 MHz) and block count, [8..12] the same for the longest per-lane job,
+ * [13] per-lane job count. */
+int bsg_engine_diag(const bsg_engine* eng, uint64_t out[16]);
 /* Last run's candidate count (diagnostics). */
 uint64_t bsg_engine_candidates(const bsg_engine* eng);
 
