@@ -20,6 +20,7 @@ LIB_PATH = os.environ.get("BSG_LIB_PATH") or os.path.join(_HERE, "libbsgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bsgpu.h")
 
 BSG_OK = 0
+READ_SLACK = 256  # BSG_READ_SLACK: readable bytes required after the last stream
 ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EDEVICE", -71: "ESTATE", -19: "ENODEV"}
 
 
@@ -189,7 +190,7 @@ class DeviceBuffer:
 
     def __init__(self, nbytes: int, device: int = 0):
         self.device, self.nbytes = device, nbytes
-        self.ptr = lib().bsg_device_malloc(device, nbytes)
+        self.ptr = lib().bsg_device_malloc(device, nbytes + READ_SLACK)
         if not self.ptr:
             raise BsgError(-12, "bsg_device_malloc")
 

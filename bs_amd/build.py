@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbsgpu.so")
-SOURCES = ["bsgpu_kernels.hip", "bsgpu_host.cpp"]
+SOURCES = ["bsgpu_kernels.hip", "bsgpu_host.cpp", "bs_split.cpp"]
 HEADERS = ["bsgpu_internal.h", "bsgpu_launch.h", "buzhash32_table.inc", "sha256_device.h"]
 ARCH = os.environ.get("BSG_OFFLOAD_ARCH", "gfx950")
 
@@ -19,6 +19,7 @@ def _stale() -> bool:
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(os.path.dirname(HERE), "include", "bsgpu.h"))
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "bs_split.hpp"))
     return any(os.path.getmtime(d) > t for d in deps)
 
 

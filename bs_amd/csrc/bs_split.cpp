@@ -1,0 +1,582 @@
+// bs_split.cpp — C++ host mirror of split.Writer / split.Reader / store/mem over libbsgpu
+// (include/bs_split.hpp), plus the C ABI wrappers the Python tests drive (bsg_memstore_*,
+// bsg_writer_*, bsg_reader_*).
+//
+// Tree assembly restates hashsplit v1.1.1's TreeBuilder as wired by split.NewWriter
+// (split/split.go:51-90): every chunk is Added with level/fanout; a level-i node closes when a
+// chunk of level > i arrives; F turns a finished TreeBuilderNode into a split.Node whose child
+// nodes are PutProto'd and whose chunks are Put. Root() folds the open levels and prunes
+// single-child roots. Parity of Root with Go is unpinned (the module's source is not in the
+// reference tree), chunk boundaries and refs are pinned by the tests.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/bs_split.hpp"
+
+namespace bs {
+
+const Ref Zero{};
+
+std::string RefString(const Ref& r) {
+  static const char* hx = "0123456789abcdef";
+  std::string s(64, '0');
+  for (int i = 0; i < 32; ++i) {
+    s[2 * i] = hx[r[i] >> 4];
+    s[2 * i + 1] = hx[r[i] & 15];
+  }
+  return s;
+}
+
+Status GpuHasher::Sum(const uint8_t* data, size_t n, Ref* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  const uint64_t off = 0, len = n;
+  static const uint8_t empty = 0;
+  int rc = bsg_sha256_batch(device_, n ? data : &empty, &off, &len, 1, out->data());
+  return rc ? Status::Err(rc, std::string("sha256: ") + bsg_errstr(rc)) : Status::Ok();
+}
+
+Status MemStore::Get(const Ref& ref, std::vector<uint8_t>* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blobs_.find(ref);
+  if (it == blobs_.end()) return Status::Err(kNotFound, "not found");
+  *out = it->second;
+  return Status::Ok();
+}
+
+Status MemStore::Put(const uint8_t* data, size_t n, Ref* ref, bool* added) {  // mem.go:62-76
+  Ref r;
+  Status s = hasher_.Sum(data, n, &r);
+  if (!s.ok()) return s;
+  if (ref) *ref = r;
+  return PutWithRef(r, data, n, added);
+}
+
+Status MemStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blobs_.find(ref);
+  bool add = it == blobs_.end();
+  if (add) blobs_.emplace(ref, std::vector<uint8_t>(data, data + n));
+  if (added) *added = add;
+  return Status::Ok();
+}
+
+Status MemStore::ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) {
+  std::vector<Ref> refs;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = blobs_.upper_bound(start); it != blobs_.end(); ++it) refs.push_back(it->first);
+  }
+  for (const Ref& r : refs) {
+    Status s = f(r);
+    if (!s.ok()) return s;
+  }
+  return Status::Ok();
+}
+
+size_t MemStore::Size() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return blobs_.size();
+}
+
+namespace split {
+
+// ---------------------------------------------------------------------------------------------
+// proto3 wire format of split.Node / split.Child, as Go's proto.Marshal writes it: fields in
+// number order, zero-valued scalars omitted, repeated messages length-delimited.
+// ---------------------------------------------------------------------------------------------
+namespace {
+void put_varint(std::string& o, uint64_t v) {
+  while (v >= 0x80) {
+    o.push_back((char)(v | 0x80));
+    v >>= 7;
+  }
+  o.push_back((char)v);
+}
+std::string child_bytes(const Child& c) {
+  std::string o;
+  o.push_back(0x0a);
+  put_varint(o, 32);
+  o.append(reinterpret_cast<const char*>(c.ref.data()), 32);
+  if (c.offset) {
+    o.push_back(0x10);
+    put_varint(o, c.offset);
+  }
+  return o;
+}
+bool get_varint(const uint8_t*& p, const uint8_t* e, uint64_t* v) {
+  uint64_t x = 0;
+  for (int s = 0; s < 64 && p < e; s += 7) {
+    const uint8_t b = *p++;
+    x |= (uint64_t)(b & 0x7f) << s;
+    if (b < 0x80) {
+      *v = x;
+      return true;
+    }
+  }
+  return false;
+}
+bool parse_child(const uint8_t* p, const uint8_t* e, Child* c) {
+  while (p < e) {
+    uint64_t tag, v;
+    if (!get_varint(p, e, &tag)) return false;
+    if (tag == 0x0a) {
+      if (!get_varint(p, e, &v) || v > (uint64_t)(e - p)) return false;
+      std::memset(c->ref.data(), 0, 32);
+      std::memcpy(c->ref.data(), p, std::min<uint64_t>(v, 32));  // bs.RefFromBytes
+      p += v;
+    } else if (tag == 0x10) {
+      if (!get_varint(p, e, &c->offset)) return false;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+}  // namespace
+
+std::string Node::Marshal() const {
+  std::string o;
+  for (const Child& c : nodes) {
+    std::string b = child_bytes(c);
+    o.push_back(0x0a);
+    put_varint(o, b.size());
+    o += b;
+  }
+  for (const Child& c : leaves) {
+    std::string b = child_bytes(c);
+    o.push_back(0x12);
+    put_varint(o, b.size());
+    o += b;
+  }
+  if (offset) {
+    o.push_back(0x18);
+    put_varint(o, offset);
+  }
+  if (size) {
+    o.push_back(0x20);
+    put_varint(o, size);
+  }
+  return o;
+}
+
+bool Node::Unmarshal(const uint8_t* p, size_t n) {
+  const uint8_t* e = p + n;
+  nodes.clear();
+  leaves.clear();
+  offset = size = 0;
+  while (p < e) {
+    uint64_t tag, v;
+    if (!get_varint(p, e, &tag)) return false;
+    if (tag == 0x0a || tag == 0x12) {
+      if (!get_varint(p, e, &v) || v > (uint64_t)(e - p)) return false;
+      Child c;
+      if (!parse_child(p, p + v, &c)) return false;
+      (tag == 0x0a ? nodes : leaves).push_back(c);
+      p += v;
+    } else if (tag == 0x18) {
+      if (!get_varint(p, e, &offset)) return false;
+    } else if (tag == 0x20) {
+      if (!get_varint(p, e, &size)) return false;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Writer
+// ---------------------------------------------------------------------------------------------
+struct Writer::Wrapped {  // split.nodeWrapper: a finished Node whose children are stored
+  Node node;
+};
+struct Writer::TBNode {   // hashsplit.TreeBuilderNode
+  std::vector<std::shared_ptr<Wrapped>> nodes;
+  std::vector<Child> chunks;  // refs (the bytes are already Put) with their lengths in offset
+  uint64_t size = 0, offset = 0;
+};
+
+std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) {
+  Status dummy;
+  if (!err) err = &dummy;
+  if (!st) {
+    *err = Status::Err(BSG_EINVAL, "nil store");
+    return nullptr;
+  }
+  std::unique_ptr<Writer> w(new Writer());
+  w->st_ = st;
+  w->rp_ = dynamic_cast<RefPutter*>(st);
+  w->opt_ = opt;
+  if (w->opt_.fanout == 0) w->opt_.fanout = 1;
+  bsg_params p;
+  p.split_bits = opt.bits;
+  p.min_size = (uint32_t)std::max(opt.min_size, 0);
+  p.fanout = w->opt_.fanout;
+  p.reserved = 0;
+  int rc = 0;
+  w->ctx_ = bsg_open(opt.device, &p, nullptr, &rc);
+  if (!w->ctx_) {
+    *err = Status::Err(rc, std::string("bsg_open: ") + bsg_errstr(rc));
+    return nullptr;
+  }
+  if (opt.tile && (rc = bsg_set_tile(w->ctx_, opt.tile))) {
+    *err = Status::Err(rc, "bsg_set_tile");
+    return nullptr;
+  }
+  *err = Status::Ok();
+  return w;
+}
+
+Writer::~Writer() {
+  if (ctx_) bsg_free(ctx_);
+}
+
+Status Writer::PutProto(const Node& node, Ref* ref) {
+  const std::string b = node.Marshal();
+  bool added;
+  return st_->Put(reinterpret_cast<const uint8_t*>(b.data()), b.size(), ref, &added);
+}
+
+Status Writer::F(TBNode& n, std::shared_ptr<Wrapped>* out) {  // split/split.go:52-81
+  auto w = std::make_shared<Wrapped>();
+  uint64_t offset = n.offset;
+  w->node.offset = n.offset;
+  w->node.size = n.size;
+  for (const auto& child : n.nodes) {
+    Ref ref;
+    Status s = PutProto(child->node, &ref);
+    if (!s.ok()) return s;
+    w->node.nodes.push_back(Child{ref, offset});
+    offset += child->node.size;
+  }
+  for (const Child& c : n.chunks) {  // chunks were Put on arrival; c.offset holds the length
+    w->node.leaves.push_back(Child{c.ref, offset});
+    offset += c.offset;
+  }
+  *out = std::move(w);
+  return Status::Ok();
+}
+
+Status Writer::Add(const Ref& ref, uint64_t len, unsigned level) {  // TreeBuilder.Add
+  if (levels_.empty()) levels_.emplace_back(new TBNode());
+  levels_[0]->chunks.push_back(Child{ref, len});
+  for (auto& n : levels_) n->size += len;
+  for (unsigned i = 0; i < level; ++i) {
+    if (i == levels_.size() - 1) {
+      auto* top = new TBNode();
+      top->size = levels_[i]->size;
+      top->offset = levels_[i]->offset;
+      levels_.emplace_back(top);
+    }
+    std::shared_ptr<Wrapped> w;
+    Status s = F(*levels_[i], &w);
+    if (!s.ok()) return s;
+    levels_[i + 1]->nodes.push_back(std::move(w));
+    auto* fresh = new TBNode();
+    fresh->offset = levels_[i + 1]->offset + levels_[i + 1]->size;
+    levels_[i].reset(fresh);
+  }
+  return Status::Ok();
+}
+
+Status Writer::Drain() {
+  const size_t n = bsg_pending(ctx_);
+  if (!n) return Status::Ok();
+  drained_.resize(n);
+  const size_t got = bsg_drain(ctx_, drained_.data(), n);
+  for (size_t i = 0; i < got; ++i) {
+    const bsg_chunk& c = drained_[i];
+    if (c.offset != base_ + head_ || c.offset + c.len > base_ + buf_.size())
+      return Status::Err(BSG_EDEVICE, "chunk records out of order");
+    const uint8_t* bytes = buf_.data() + head_;
+    Ref ref;
+    std::memcpy(ref.data(), c.ref, 32);
+    bool added;
+    Status s = rp_ ? rp_->PutWithRef(ref, bytes, c.len, &added)  // GPU ref, no re-hash
+                   : st_->Put(bytes, c.len, &ref, &added);       // store computes the ref
+    if (!s.ok()) return s;
+    head_ += c.len;
+    s = Add(ref, c.len, c.level / opt_.fanout);  // split/split.go:86
+    if (!s.ok()) return s;
+  }
+  if (head_ > (1u << 20) && head_ * 2 > buf_.size()) {  // compact the emitted prefix
+    buf_.erase(buf_.begin(), buf_.begin() + head_);
+    base_ += head_;
+    head_ = 0;
+  }
+  return Status::Ok();
+}
+
+Status Writer::Write(const uint8_t* p, size_t n, size_t* written) {
+  if (written) *written = 0;
+  if (closed_) return Status::Err(BSG_ESTATE, "write after close");
+  if (!sticky_.ok()) return sticky_;
+  buf_.insert(buf_.end(), p, p + n);
+  int rc = bsg_write(ctx_, p, n);
+  if (rc) return sticky_ = Status::Err(rc, std::string("bsg_write: ") + bsg_errstr(rc));
+  Status s = Drain();
+  if (!s.ok()) return sticky_ = s;
+  if (written) *written = n;
+  return Status::Ok();
+}
+
+Status Writer::Close() {  // split/split.go:104-126
+  if (closed_) return sticky_;
+  closed_ = true;
+  if (!sticky_.ok()) return sticky_;
+  int rc = bsg_close(ctx_);
+  if (rc) return sticky_ = Status::Err(rc, std::string("bsg_close: ") + bsg_errstr(rc));
+  Status s = Drain();
+  if (!s.ok()) return sticky_ = s;
+  if (levels_.empty()) return Status::Ok();  // no input: Root stays bs.Zero
+  // TreeBuilder.Root(): fold every non-empty level below the top into its parent
+  for (size_t i = 0; i + 1 < levels_.size(); ++i) {
+    TBNode& n = *levels_[i];
+    if (n.chunks.empty() && n.nodes.empty()) continue;
+    std::shared_ptr<Wrapped> w;
+    if (!(s = F(n, &w)).ok()) return sticky_ = s;
+    levels_[i + 1]->nodes.push_back(std::move(w));
+  }
+  std::shared_ptr<Wrapped> root;
+  if (levels_.size() == 1) {
+    if (!(s = F(*levels_[0], &root)).ok()) return sticky_ = s;
+  } else {
+    TBNode& top = *levels_.back();
+    if (top.nodes.size() > 1) {
+      if (!(s = F(top, &root)).ok()) return sticky_ = s;
+    } else {
+      root = top.nodes[0];  // prune would-be roots with a single child
+      while (root->node.nodes.size() == 1) {
+        std::vector<uint8_t> b;
+        if (!(s = st_->Get(root->node.nodes[0].ref, &b)).ok()) return sticky_ = s;
+        auto next = std::make_shared<Wrapped>();
+        if (!next->node.Unmarshal(b.data(), b.size()))
+          return sticky_ = Status::Err(BSG_EINVAL, "bad tree node");
+        root = next;
+      }
+    }
+  }
+  s = PutProto(root->node, &root_);
+  if (!s.ok()) return sticky_ = s;
+  levels_.clear();
+  return Status::Ok();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Reader (split/split.go:173-303)
+// ---------------------------------------------------------------------------------------------
+namespace {
+Status get_node(Store* g, const Ref& ref, Node* n) {
+  std::vector<uint8_t> b;
+  Status s = g->Get(ref, &b);
+  if (!s.ok()) return s;
+  if (!n->Unmarshal(b.data(), b.size())) return Status::Err(BSG_EINVAL, "bad tree node");
+  return Status::Ok();
+}
+}  // namespace
+
+std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err) {
+  Status dummy;
+  if (!err) err = &dummy;
+  Node n;
+  Status s = get_node(g, root, &n);
+  if (!s.ok()) {
+    *err = Status::Err(s.code, "getting root ref " + RefString(root) + ": " + s.msg);
+    return nullptr;
+  }
+  std::unique_ptr<Reader> r(new Reader());
+  r->g_ = g;
+  r->stack_.push_back(std::move(n));
+  *err = Status::Ok();
+  return r;
+}
+
+Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
+  *got = 0;
+  *eof = false;
+  while (len > 0) {
+    for (;;) {  // unwind to a node containing pos
+      const Node& node = stack_.back();
+      if (pos_ >= node.offset && pos_ < node.offset + node.size) break;
+      if (stack_.size() == 1) {
+        *eof = true;
+        return Status::Ok();
+      }
+      stack_.pop_back();
+    }
+    for (;;) {  // descend to the leaf node
+      const Node& node = stack_.back();
+      if (!node.leaves.empty()) break;
+      size_t index = 0;
+      if (pos_ > node.offset) {
+        index = std::upper_bound(node.nodes.begin(), node.nodes.end(), pos_,
+                                 [](uint64_t p, const Child& c) { return c.offset > p; }) -
+                node.nodes.begin();
+        index--;
+      }
+      Node child;
+      Status s = get_node(g_, node.nodes[index].ref, &child);
+      if (!s.ok()) return Status::Err(s.code, "getting tree node: " + s.msg);
+      stack_.push_back(std::move(child));
+    }
+    const std::vector<Child>& leaves = stack_.back().leaves;
+    size_t k = 0;
+    while (leaves.size() - k > 1 && leaves[k + 1].offset <= pos_) ++k;
+    for (; k < leaves.size() && len > 0; ++k) {
+      std::vector<uint8_t> chunk;
+      Status s = g_->Get(leaves[k].ref, &chunk);
+      if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
+      const uint64_t skip = pos_ - leaves[k].offset;
+      const size_t avail = chunk.size() - (size_t)skip;
+      const size_t take = std::min(avail, len);
+      std::memcpy(buf, chunk.data() + skip, take);
+      buf += take;
+      len -= take;
+      *got += take;
+      pos_ += take;
+      if (take < avail) return Status::Ok();
+    }
+  }
+  return Status::Ok();
+}
+
+uint64_t Reader::Seek(int64_t offset, int whence) {
+  switch (whence) {
+    case 0: pos_ = (uint64_t)offset; break;
+    case 1: pos_ = (uint64_t)((int64_t)pos_ + offset); break;
+    case 2: pos_ = (uint64_t)((int64_t)stack_.front().size + offset); break;
+    default: break;
+  }
+  return pos_;
+}
+
+}  // namespace split
+}  // namespace bs
+
+// ---------------------------------------------------------------------------------------------
+// C ABI wrappers (bsgpu.h) so the Python tests can drive the C++ host mirror.
+// ---------------------------------------------------------------------------------------------
+struct bsg_store {
+  bs::MemStore mem;
+  explicit bsg_store(int device) : mem(device) {}
+};
+struct bsg_writer {
+  std::unique_ptr<bs::split::Writer> w;
+};
+struct bsg_reader {
+  std::unique_ptr<bs::split::Reader> r;
+};
+
+extern "C" {
+
+bsg_store* bsg_memstore_new(int device) { return new (std::nothrow) bsg_store(device); }
+void bsg_store_free(bsg_store* s) { delete s; }
+size_t bsg_store_count(const bsg_store* s) { return s ? s->mem.Size() : 0; }
+
+int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n) {
+  if (!s || !ref || !n) return BSG_EINVAL;
+  bs::Ref r;
+  std::memcpy(r.data(), ref, 32);
+  std::vector<uint8_t> b;
+  bs::Status st = s->mem.Get(r, &b);
+  if (!st.ok()) return st.code;
+  *n = b.size();
+  if (out) std::memcpy(out, b.data(), std::min(cap, b.size()));
+  return BSG_OK;
+}
+
+int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[32], int* added) {
+  if (!s || (!data && n)) return BSG_EINVAL;
+  bs::Ref r;
+  bool a = false;
+  bs::Status st = s->mem.Put(data, n, &r, &a);
+  if (!st.ok()) return st.code;
+  if (ref_out) std::memcpy(ref_out, r.data(), 32);
+  if (added) *added = a ? 1 : 0;
+  return BSG_OK;
+}
+
+size_t bsg_store_list(bsg_store* s, uint8_t* refs, size_t cap) {
+  if (!s) return 0;
+  size_t k = 0;
+  s->mem.ListRefs(bs::Zero, [&](const bs::Ref& r) {
+    if (k < cap && refs) std::memcpy(refs + 32 * k, r.data(), 32);
+    ++k;
+    return bs::Status::Ok();
+  });
+  return k;  // note: bs::Zero itself is never listed (ListRefs starts after `start`)
+}
+
+bsg_writer* bsg_writer_new(int device, bsg_store* s, const bsg_params* params, size_t tile,
+                           int* err) {
+  int dummy;
+  if (!err) err = &dummy;
+  if (!s) {
+    *err = BSG_EINVAL;
+    return nullptr;
+  }
+  bs::split::Options o;
+  if (params) {
+    o.bits = params->split_bits;
+    o.min_size = (int)params->min_size;
+    o.fanout = params->fanout;
+  }
+  o.device = device;
+  o.tile = tile;
+  bs::Status st;
+  auto w = bs::split::Writer::New(&s->mem, o, &st);
+  if (!w) {
+    *err = st.code;
+    return nullptr;
+  }
+  *err = BSG_OK;
+  return new bsg_writer{std::move(w)};
+}
+
+int bsg_writer_write(bsg_writer* w, const uint8_t* p, size_t n) {
+  if (!w) return BSG_EINVAL;
+  return w->w->Write(p, n).code;
+}
+int bsg_writer_close(bsg_writer* w) { return w ? w->w->Close().code : BSG_EINVAL; }
+int bsg_writer_root(const bsg_writer* w, uint8_t out[32]) {
+  if (!w || !out) return BSG_EINVAL;
+  std::memcpy(out, w->w->Root().data(), 32);
+  return BSG_OK;
+}
+void bsg_writer_free(bsg_writer* w) { delete w; }
+
+bsg_reader* bsg_reader_new(bsg_store* s, const uint8_t root[32], int* err) {
+  int dummy;
+  if (!err) err = &dummy;
+  if (!s || !root) {
+    *err = BSG_EINVAL;
+    return nullptr;
+  }
+  bs::Ref r;
+  std::memcpy(r.data(), root, 32);
+  bs::Status st;
+  auto rd = bs::split::Reader::New(&s->mem, r, &st);
+  if (!rd) {
+    *err = st.code;
+    return nullptr;
+  }
+  *err = BSG_OK;
+  return new bsg_reader{std::move(rd)};
+}
+
+int64_t bsg_reader_read(bsg_reader* r, uint8_t* buf, size_t n) {
+  if (!r || (!buf && n)) return BSG_EINVAL;
+  size_t got = 0;
+  bool eof = false;
+  bs::Status st = r->r->Read(buf, n, &got, &eof);
+  if (!st.ok()) return st.code;
+  return (int64_t)got;
+}
+int64_t bsg_reader_seek(bsg_reader* r, int64_t off, int whence) {
+  return r ? (int64_t)r->r->Seek(off, whence) : BSG_EINVAL;
+}
+uint64_t bsg_reader_size(const bsg_reader* r) { return r ? r->r->Size() : 0; }
+void bsg_reader_free(bsg_reader* r) { delete r; }
+
+}  // extern "C"

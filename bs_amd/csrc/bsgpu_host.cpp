@@ -338,7 +338,7 @@ struct bsg_ctx {
 
   int process(bool final_seg) {
     if (fill == 0 && !final_seg) return BSG_OK;
-    HCHECK(dtile.ensure(fill));
+    HCHECK(dtile.ensure(fill + kReadSlack));
     if (fill) HCHECK(hipMemcpyAsync(dtile.p, staging.p, fill, hipMemcpyHostToDevice, eng->stream));
     StreamDesc d{};
     d.data_off = 0;
@@ -482,6 +482,25 @@ int bsg_engine_run(bsg_engine* e, const uint8_t* d_data, const uint64_t* off, co
   int rc = normalize(params, &p, nullptr);
   if (rc) return rc;
   if ((rc = e->setdev())) return rc;
+  // the SHA-256 loader reads up to kReadSlack bytes past a stream's end (masked): that memory
+  // must belong to the same allocation
+  uint64_t hi = 0;
+  for (uint32_t s = 0; s < nstreams; ++s) hi = std::max<uint64_t>(hi, off[s] + len[s]);
+  if (nstreams) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_data) != hipSuccess) {
+      (void)hipGetLastError();
+      return BSG_EINVAL;  // not a HIP device allocation
+    }
+    const uint64_t avail = (uint64_t)((const uint8_t*)base + size - d_data);
+    if (hi + kReadSlack > avail) {
+      std::fprintf(stderr, "bsgpu: device buffer needs %llu readable bytes after the last "
+                           "stream (has %llu)\n", (unsigned long long)kReadSlack,
+                   (unsigned long long)(avail > hi ? avail - hi : 0));
+      return BSG_EINVAL;
+    }
+  }
   e->descs.assign(nstreams, StreamDesc{});
   for (uint32_t s = 0; s < nstreams; ++s) {
     if (off[s] % 16 != 0 || len[s] >= (1ull << 40)) return BSG_EINVAL;
@@ -670,7 +689,7 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
     total += (len[s] + 15) & ~15ull;
   }
   DevBuf d;
-  if (d.ensure(total) != hipSuccess) {
+  if (d.ensure(total + kReadSlack) != hipSuccess) {
     bsg_engine_destroy(e);
     return BSG_ENOMEM;
   }
@@ -749,14 +768,14 @@ int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const
     (void)hipGetLastError();
   uint64_t hi = 0;
   for (uint32_t i = 0; i < n; ++i) hi = std::max<uint64_t>(hi, off[i] + len[i]);
+  // always hash from a private copy with kReadSlack bytes of tail padding
   DevBuf dd, doff, dlen, drefs;
   int rc = BSG_OK;
-  const uint8_t* dbase = base;
-  if (!on_device) {
-    if (dd.ensure(hi) != hipSuccess) return BSG_ENOMEM;
-    if (hi && hipMemcpy(dd.p, base, hi, hipMemcpyHostToDevice) != hipSuccess) rc = BSG_EDEVICE;
-    dbase = dd.as<uint8_t>();
-  }
+  if (dd.ensure(hi + kReadSlack) != hipSuccess) return BSG_ENOMEM;
+  if (hi && hipMemcpy(dd.p, base, hi, on_device ? hipMemcpyDeviceToDevice
+                                                : hipMemcpyHostToDevice) != hipSuccess)
+    rc = BSG_EDEVICE;
+  const uint8_t* dbase = dd.as<uint8_t>();
   if (rc == BSG_OK && (doff.ensure(8ull * n) != hipSuccess || dlen.ensure(8ull * n) != hipSuccess ||
                        drefs.ensure(32ull * n) != hipSuccess))
     rc = BSG_ENOMEM;

@@ -99,5 +99,6 @@ static_assert(sizeof(Counters) == 256, "Counters layout");
 constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave-per-chunk path below 64 KiB
 constexpr int kLongRow = 68;               // LDS words per K+W row (64 + pad: conflict-free b128)
 constexpr int kLptBuckets = 4096;          // longest-first job order: counting sort on nblocks
+constexpr uint64_t kReadSlack = 256;       // readable bytes required after every stream's data
 
 }  // namespace bsg

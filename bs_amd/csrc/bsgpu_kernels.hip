@@ -480,25 +480,28 @@ typedef __attribute__((address_space(1))) const uint32_t gu32;
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
 // Block at message offset o0 (>= prefix) of a job whose data bytes are dbase[o - prefix].
-// Branch-free on purpose: the same 17 dword loads into the same registers every time, so the
-// compiler never has to drain a prefetch at a control-flow join. Every load is in bounds: a
-// dword holding at least one valid byte never crosses a page, dwords past the valid range are
-// clamped onto the last one holding a valid byte, and a block with no data bytes reads the
-// always-valid `safe` address instead (its bytes are masked off by pad_words).
+// Branch-free on purpose (the same five loads into the same registers every time, so the
+// compiler never drains a prefetch at a control-flow join) and wide (4 x dwordx4 + 1 dword:
+// every load instruction touches one cache line per lane, so fewer instructions = less
+// TA/L1 work when four waves share a CU). Reads may run up to kReadSlack bytes past the end of
+// the data; the engine requires that much readable memory after every stream
+// (bsg_engine_run checks the allocation), and pad_words masks whatever is read there.
 __device__ __forceinline__ void raw_load(const uint8_t* dbase, uint64_t o0, uint32_t prefix,
-                                         uint64_t L, const void* safe, RawBlock& rb) {
+                                         uint64_t L, RawBlock& rb) {
   const uint8_t* p = dbase + (o0 - prefix);
   const int64_t vv = (int64_t)L - (int64_t)o0;
-  const int32_t v = vv < 0 ? -1 : (vv >= 64 ? 64 : (int32_t)vv);
-  const uintptr_t addr = v > 0 ? reinterpret_cast<uintptr_t>(p)
-                               : reinterpret_cast<uintptr_t>(safe) & ~(uintptr_t)3;
+  rb.valid = vv < 0 ? -1 : (vv >= 64 ? 64 : (int32_t)vv);
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
   const uint32_t sh = (uint32_t)(addr & 3u);
   gu32* al = reinterpret_cast<gu32*>(addr & ~(uintptr_t)3);
-  const uint32_t jmax = v > 0 ? ((uint32_t)v + sh - 1) >> 2 : 0u;
   rb.sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
-  rb.valid = v;
+  gu32x4* q = reinterpret_cast<gu32x4*>(al);
 #pragma unroll
-  for (int j = 0; j < 17; ++j) rb.r[j] = al[min((uint32_t)j, jmax)];
+  for (int i = 0; i < 4; ++i) {
+    const u32x4 x = q[i];
+    rb.r[4 * i] = x.x; rb.r[4 * i + 1] = x.y; rb.r[4 * i + 2] = x.z; rb.r[4 * i + 3] = x.w;
+  }
+  rb.r[16] = al[16];
 }
 
 __device__ __forceinline__ void raw_to_words(const RawBlock& rb, uint32_t (&W)[16]) {
@@ -515,12 +518,6 @@ __device__ __forceinline__ void pad_words(int32_t valid, uint32_t (&W)[16]) {
     const uint32_t pad = (k >= 0 && k < 4) ? (0x80u << (24 - 8 * k)) : 0u;
     W[q] = (W[q] & keep) | pad;
   }
-}
-
-__device__ __forceinline__ void sha_load_fast(const uint8_t* p, uint32_t (&W)[16]) {
-  RawBlock rb;
-  raw_load(p, 0, 0, 64, p, rb);
-  raw_to_words(rb, W);
 }
 
 __device__ __forceinline__ void sha_load_slow(const ShaJob& jb, uint32_t blk, uint32_t (&W)[16]) {
@@ -594,7 +591,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
           sha_finish(a, jb, st);
         } else {
           has = true;
-          if (jb.prefix == 0) raw_load(jb.dbase, 0, 0, jb.L, a.streams, rb);
+          if (jb.prefix == 0) raw_load(jb.dbase, 0, 0, jb.L, rb);
         }
       }
     }
@@ -614,9 +611,9 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
     } else {
       sha_load_slow(jb, blk, W);  // head block of a continued chunk (once per segment)
     }
-    // prefetch the next block, unconditionally (past the last block it reads the safe
-    // address): a branch here would make the compiler drain vmcnt at the join
-    raw_load(jb.dbase, o0 + 64, jb.prefix, jb.L, a.streams, rb);
+    // prefetch the next block, unconditionally (past the last block it reads slack bytes,
+    // which are never used): a branch here would make the compiler drain vmcnt at the join
+    raw_load(jb.dbase, o0 + 64, jb.prefix, jb.L, rb);
     sha256_compress(st, W);
     if (++blk == jb.nblocks) {
       sha_finish(a, jb, st);
@@ -751,10 +748,11 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t
   }
   const uint32_t nblocks = __builtin_amdgcn_readfirstlane(jb.nblocks);
   for (uint32_t base = 0; base < nblocks; base += 64) {
-    // phase A: lane i expands block base+i into K+W (LDS row i)
-    const uint32_t blk = base + lane;
+    // phase A: lane i expands block base+i into K+W (LDS row i); lanes past the last block
+    // re-expand the last block (their rows are never read) so no load leaves the slack zone
+    const uint32_t blk = min(base + lane, nblocks - 1);
     RawBlock rb;
-    raw_load(jb.dbase, 64ull * blk, 0, jb.L, a.streams, rb);
+    raw_load(jb.dbase, 64ull * blk, 0, jb.L, rb);
     uint32_t W[16];
     raw_to_words(rb, W);
     if (rb.valid < 64) {
@@ -869,7 +867,7 @@ __global__ __launch_bounds__(256) void k_sha_blobs(BlobShaArgs a) {
     uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                       0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
     RawBlock rb;
-    raw_load(jb.dbase, 0, 0, jb.L, a.off, rb);
+    raw_load(jb.dbase, 0, 0, jb.L, rb);
     for (uint32_t blk = 0; blk < jb.nblocks; ++blk) {
       uint32_t W[16];
       raw_to_words(rb, W);
@@ -881,7 +879,7 @@ __global__ __launch_bounds__(256) void k_sha_blobs(BlobShaArgs a) {
           W[15] = (uint32_t)bits;
         }
       }
-      raw_load(jb.dbase, 64ull * (blk + 1), 0, jb.L, a.off, rb);
+      raw_load(jb.dbase, 64ull * (blk + 1), 0, jb.L, rb);
       sha256_compress(st, W);
     }
     uint32_t* ref = reinterpret_cast<uint32_t*>(a.refs + 32 * i);

@@ -1,0 +1,164 @@
+// bs_split.hpp — C++ host mirror of the reference's split package and Store surface, built on
+// libbsgpu's C ABI (include/bsgpu.h). Same names, argument meaning and error behaviour as the
+// Go originals; the per-byte chunking and every SHA-256 run on the GPU.
+//
+//   bs::Ref / bs::Zero / RefString        bs.go:12-36
+//   bs::Store (Get / Put / ListRefs)       store.go:9-42
+//   bs::RefPutter (optional, like MultiPutter store.go:44-47): Put with a ref the caller already
+//                 computed on the GPU, so a backend need not hash the blob again
+//   bs::MemStore                           store/mem/mem.go:17-124
+//   bs::split::Writer  New/Write/Close/Root, options Bits/MinSize/Fanout   split/split.go:30-165
+//   bs::split::Reader  New/Read/Seek/Size                                  split/split.go:173-303
+//   bs::split::Node / Child (proto3 wire format)                           split/split.proto:6-26
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bsgpu.h"
+
+namespace bs {
+
+using Ref = std::array<uint8_t, 32>;
+extern const Ref Zero;  // bs.Zero
+std::string RefString(const Ref& r);  // lowercase hex (bs.go:29-31)
+inline bool RefLess(const Ref& a, const Ref& b) { return a < b; }  // bs.go:34-36
+
+// Go `error` -> Status: code 0 is nil; other codes are BSG_* (bsgpu.h) or kNotFound.
+struct Status {
+  int code = 0;
+  std::string msg;
+  bool ok() const { return code == 0; }
+  static Status Ok() { return Status{}; }
+  static Status Err(int c, std::string m) { return Status{c, std::move(m)}; }
+};
+constexpr int kNotFound = -2;  // bs.ErrNotFound (store.go:63)
+
+class Store {
+ public:
+  virtual ~Store() = default;
+  virtual Status Get(const Ref& ref, std::vector<uint8_t>* out) = 0;
+  // Put adds the blob if absent; *ref = its SHA-256, *added = whether it was new.
+  virtual Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) = 0;
+  // Calls f for each ref > start in lexicographic order (store.go:21-23).
+  virtual Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) = 0;
+};
+
+class RefPutter {
+ public:
+  virtual ~RefPutter() = default;
+  virtual Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) = 0;
+};
+
+// Batched/one-off SHA-256 of host bytes on the GPU (persistent device buffers + stream).
+class GpuHasher {
+ public:
+  explicit GpuHasher(int device = 0) : device_(device) {}
+  Status Sum(const uint8_t* data, size_t n, Ref* out);
+
+ private:
+  int device_;
+  std::mutex mu_;
+};
+
+class MemStore : public Store, public RefPutter {
+ public:
+  explicit MemStore(int device = 0) : hasher_(device) {}
+  Status Get(const Ref& ref, std::vector<uint8_t>* out) override;
+  Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) override;
+  Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
+  Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
+  size_t Size() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::map<Ref, std::vector<uint8_t>> blobs_;
+  GpuHasher hasher_;
+};
+
+namespace split {
+
+struct Child {  // split.proto Child {bytes ref = 1; uint64 offset = 2;}
+  Ref ref{};
+  uint64_t offset = 0;
+};
+struct Node {  // split.proto Node {nodes = 1; leaves = 2; offset = 3; size = 4;}
+  std::vector<Child> nodes, leaves;
+  uint64_t offset = 0, size = 0;
+  std::string Marshal() const;                    // deterministic proto3, as Go proto.Marshal
+  bool Unmarshal(const uint8_t* p, size_t n);
+};
+
+// split.Option values (split/split.go:128-165).
+struct Options {
+  unsigned bits = 16;     // Bits(n)
+  int min_size = 1024;    // MinSize(n)
+  unsigned fanout = 8;    // Fanout(n)
+  int device = 0;         // HIP device that runs the chunker and the hashes
+  size_t tile = 0;        // staging tile in bytes (0: library default, 256 MiB)
+};
+inline Options Bits(Options o, unsigned n) { o.bits = n; return o; }
+inline Options MinSize(Options o, int n) { o.min_size = n; return o; }
+inline Options Fanout(Options o, unsigned n) { o.fanout = n; return o; }
+
+class Writer {
+ public:
+  // split.NewWriter(ctx, st, opts...). The store must outlive the Writer.
+  static std::unique_ptr<Writer> New(Store* st, const Options& opt, Status* err);
+  ~Writer();
+  // io.Writer: consumes all of p (copied); chunks found so far are Put to the store.
+  Status Write(const uint8_t* p, size_t n, size_t* written = nullptr);
+  // Flushes the final chunk, builds the tree root; Root() is valid afterwards. Idempotent.
+  Status Close();
+  const Ref& Root() const { return root_; }
+
+  struct TBNode;
+  struct Wrapped;
+
+ private:
+  Writer() = default;
+  Status Drain();
+  Status Add(const Ref& ref, uint64_t len, unsigned level);  // hashsplit TreeBuilder.Add
+  Status F(TBNode& n, std::shared_ptr<Wrapped>* out);        // split.go:52-81
+  Status PutProto(const Node& node, Ref* ref);               // proto.go:22-29
+
+  Store* st_ = nullptr;
+  RefPutter* rp_ = nullptr;
+  Options opt_;
+  bsg_ctx* ctx_ = nullptr;
+  std::vector<uint8_t> buf_;  // stream bytes not yet emitted as chunks
+  size_t head_ = 0;           // emitted prefix of buf_
+  uint64_t base_ = 0;         // stream offset of buf_[0]
+  std::vector<std::unique_ptr<TBNode>> levels_;
+  std::vector<bsg_chunk> drained_;
+  Ref root_{};
+  bool closed_ = false;
+  Status sticky_;
+};
+
+class Reader {
+ public:
+  // split.NewReader(ctx, g, ref)
+  static std::unique_ptr<Reader> New(Store* g, const Ref& root, Status* err);
+  // io.Reader: returns bytes read; 0 with *eof = true at the end.
+  Status Read(uint8_t* buf, size_t n, size_t* got, bool* eof);
+  // io.Seeker (whence: 0 start, 1 current, 2 end).
+  uint64_t Seek(int64_t offset, int whence);
+  uint64_t Size() const { return stack_.front().size; }
+
+ private:
+  Reader() = default;
+  Store* g_ = nullptr;
+  uint64_t pos_ = 0;
+  std::vector<Node> stack_;  // stack_[0] is the root
+};
+
+}  // namespace split
+}  // namespace bs

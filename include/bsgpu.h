@@ -87,7 +87,10 @@ typedef struct bsg_engine bsg_engine;
 bsg_engine* bsg_engine_create(int device, const uint32_t* table /* 256 or NULL */, int* err);
 void bsg_engine_destroy(bsg_engine* eng);
 /* Enqueue split + hash of nstreams streams d_data[off[i] .. off[i]+len[i]) (device memory,
- * off[i] % 16 == 0; off/len are host arrays). Asynchronous on the engine's stream. */
+ * off[i] % 16 == 0; off/len are host arrays). Asynchronous on the engine's stream.
+ * The allocation holding d_data must extend at least BSG_READ_SLACK bytes past the end of the
+ * last stream (the SHA-256 loader reads whole 64-byte blocks and masks the excess). */
+#define BSG_READ_SLACK 256
 int bsg_engine_run(bsg_engine* eng, const uint8_t* d_data, const uint64_t* off,
                    const uint64_t* len, uint32_t nstreams, const bsg_params* params);
 /* Wait for the run; handles candidate-buffer growth (re-runs once if needed). Returns the
@@ -135,6 +138,33 @@ int bsg_device_synchronize(int device);
 /* Utility (benchmarks/tests, not part of the reference surface): fill device memory with the
  * SplitMix64 counter stream of bs_amd/synth.py (word i = splitmix64(seed + (i+1)*0x9E37...)). */
 int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed, void* stream);
+
+/* ---- C++ host mirror of split.Writer / split.Reader / store/mem (bs_split.hpp), exposed for
+ * C callers and tests ---- */
+typedef struct bsg_store bsg_store;   /* store/mem (store/mem/mem.go:17-124); refs via GPU */
+bsg_store* bsg_memstore_new(int device);
+void bsg_store_free(bsg_store* s);
+size_t bsg_store_count(const bsg_store* s);
+/* Get: copies min(cap, len) bytes, *n = blob length; returns kNotFound (-2) if absent. */
+int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n);
+int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[32], int* added);
+/* All refs in lexicographic order (32 bytes each, up to cap); returns the total count. */
+size_t bsg_store_list(bsg_store* s, uint8_t* refs, size_t cap);
+
+typedef struct bsg_writer bsg_writer; /* split.NewWriter / Write / Close / Root */
+bsg_writer* bsg_writer_new(int device, bsg_store* s, const bsg_params* params, size_t tile,
+                           int* err);
+int bsg_writer_write(bsg_writer* w, const uint8_t* p, size_t n);
+int bsg_writer_close(bsg_writer* w);
+int bsg_writer_root(const bsg_writer* w, uint8_t out[32]);
+void bsg_writer_free(bsg_writer* w);
+
+typedef struct bsg_reader bsg_reader; /* split.NewReader / Read / Seek / Size */
+bsg_reader* bsg_reader_new(bsg_store* s, const uint8_t root[32], int* err);
+int64_t bsg_reader_read(bsg_reader* r, uint8_t* buf, size_t n); /* bytes; 0 at EOF; <0 error */
+int64_t bsg_reader_seek(bsg_reader* r, int64_t off, int whence);
+uint64_t bsg_reader_size(const bsg_reader* r);
+void bsg_reader_free(bsg_reader* r);
 
 #ifdef __cplusplus
 }

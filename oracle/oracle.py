@@ -199,3 +199,158 @@ def py_split(table, data: bytes, bits: int = 16, min_size: int = 1024) -> list[P
         out.append(PyChunk(start, len(data) - start, tz - bits if tz >= bits else 0,
                            hashlib.sha256(data[start:]).digest()))
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Tree + Root restatement (split.Writer.Close -> Root). Parity vs Go is UNPINNED: hashsplit's
+# TreeBuilder (v1.1.1) is restated from its published source as recalled; see DESIGN.md.
+#   split/split.go:51-83   F: PutProto child nodes, Put chunks, Node{Offset, Size, Nodes, Leaves}
+#   split/split.go:85-87   tb.Add(chunk, level / fanout)
+#   split/split.go:104-126 Close: tb.Root(); PutProto(root) -> Root (zero ref if no input)
+#   split/split.proto:6-26 Node {nodes=1, leaves=2, offset=3, size=4}; Child {ref=1, offset=2}
+# ---------------------------------------------------------------------------------------------
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        if v:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def proto_child(ref: bytes, offset: int) -> bytes:
+    out = b"\x0a" + _varint(len(ref)) + ref if ref else b""
+    if offset:
+        out += b"\x10" + _varint(offset)
+    return out
+
+
+def proto_node(nodes, leaves, offset: int, size: int) -> bytes:
+    """proto3 wire format as Go's proto.Marshal emits it (field order, zero values omitted)."""
+    out = bytearray()
+    for ref, off in nodes:
+        c = proto_child(ref, off)
+        out += b"\x0a" + _varint(len(c)) + c
+    for ref, off in leaves:
+        c = proto_child(ref, off)
+        out += b"\x12" + _varint(len(c)) + c
+    if offset:
+        out += b"\x18" + _varint(offset)
+    if size:
+        out += b"\x20" + _varint(size)
+    return bytes(out)
+
+
+class _TBNode:
+    def __init__(self, offset=0, size=0):
+        self.nodes, self.chunks, self.offset, self.size = [], [], offset, size
+
+
+class _Wrapped:  # split.nodeWrapper: a finished Node (its children already stored)
+    def __init__(self, nodes, leaves, offset, size):
+        self.nodes, self.leaves, self.offset, self.size = nodes, leaves, offset, size
+
+    def proto(self) -> bytes:
+        return proto_node(self.nodes, self.leaves, self.offset, self.size)
+
+
+def py_tree_root(chunks, fanout: int = 8, store: dict | None = None) -> bytes:
+    """chunks: iterable of (chunk_bytes, level) in stream order; returns Writer.Root (32 bytes).
+    Chunk refs are SHA-256 of their bytes (bs.go:24-26). If `store` is given (a dict), every
+    Put lands in it (ref -> blob), like store/mem."""
+    store = {} if store is None else store
+
+    def put(b: bytes) -> bytes:
+        r = hashlib.sha256(b).digest()
+        store[r] = b
+        return r
+
+    def F(n: _TBNode) -> _Wrapped:  # split/split.go:52-81
+        off = n.offset
+        nodes, leaves = [], []
+        for child in n.nodes:
+            nodes.append((put(child.proto()), off))
+            off += child.size
+        for ref, ln in n.chunks:
+            leaves.append((ref, off))
+            off += ln
+        return _Wrapped(nodes, leaves, n.offset, n.size)
+
+    levels: list[_TBNode] = []
+    for data, level in chunks:  # hashsplit TreeBuilder.Add(bytes, level / fanout)
+        ln = len(data)
+        ref = put(bytes(data))
+        level //= fanout
+        if not levels:
+            levels.append(_TBNode())
+        levels[0].chunks.append((ref, ln))
+        for n in levels:
+            n.size += ln
+        for i in range(level):
+            if i == len(levels) - 1:
+                levels.append(_TBNode(offset=levels[i].offset, size=levels[i].size))
+            levels[i + 1].nodes.append(F(levels[i]))
+            levels[i] = _TBNode(offset=levels[i + 1].offset + levels[i + 1].size)
+    if not levels:
+        return bytes(32)  # Root stays bs.Zero (split_test.go:15-25)
+    # Root(): fold every non-empty level below the top into its parent
+    for i in range(len(levels) - 1):
+        if levels[i].chunks or levels[i].nodes:
+            levels[i + 1].nodes.append(F(levels[i]))
+    if len(levels) == 1:
+        root = F(levels[0])
+    else:
+        top = levels[-1]
+        if len(top.nodes) > 1:
+            root = F(top)
+        else:
+            root = top.nodes[0]  # prune single-child roots (their F already ran)
+            while len(root.nodes) == 1:
+                root = _Wrapped(*_unwrap(store, root.nodes[0][0]))
+    return put(root.proto())
+
+
+def _unwrap(store, ref):
+    """Decode a stored Node proto back into (nodes, leaves, offset, size)."""
+    b = store[ref]
+    nodes, leaves, offset, size = [], [], 0, 0
+    i = 0
+
+    def varint(i):
+        v, s = 0, 0
+        while True:
+            c = b[i]; i += 1
+            v |= (c & 0x7F) << s
+            s += 7
+            if c < 0x80:
+                return v, i
+    while i < len(b):
+        tag, i = varint(i)
+        f, wt = tag >> 3, tag & 7
+        if wt == 2:
+            ln, i = varint(i)
+            sub = b[i:i + ln]; i += ln
+            r, o, j = b"", 0, 0
+            while j < len(sub):
+                t2, j2 = sub[j], j + 1
+                if t2 == 0x0a:
+                    l2 = sub[j2]; r = bytes(sub[j2 + 1:j2 + 1 + l2]); j = j2 + 1 + l2
+                else:
+                    v, s, j = 0, 0, j2
+                    while True:
+                        c = sub[j]; j += 1
+                        v |= (c & 0x7F) << s; s += 7
+                        if c < 0x80:
+                            break
+                    o = v
+            (nodes if f == 1 else leaves).append((r, o))
+        else:
+            v, i = varint(i)
+            if f == 3:
+                offset = v
+            else:
+                size = v
+    return nodes, leaves, offset, size
