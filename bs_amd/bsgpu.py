@@ -96,6 +96,25 @@ def lib() -> ctypes.CDLL:
         "bsg_device_free": (ctypes.c_int, [ctypes.c_int, vp]),
         "bsg_memcpy": (ctypes.c_int, [ctypes.c_int, vp, vp, ctypes.c_size_t, ctypes.c_int]),
         "bsg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
+        "bsg_memstore_new": (vp, [ctypes.c_int]),
+        "bsg_store_free": (None, [vp]),
+        "bsg_store_count": (ctypes.c_size_t, [vp]),
+        "bsg_store_get": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t,
+                                         ctypes.POINTER(ctypes.c_size_t)]),
+        "bsg_store_put": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp,
+                                         ctypes.POINTER(ctypes.c_int)]),
+        "bsg_store_list": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
+        "bsg_writer_new": (vp, [ctypes.c_int, vp, ctypes.POINTER(Params), ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_int)]),
+        "bsg_writer_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
+        "bsg_writer_close": (ctypes.c_int, [vp]),
+        "bsg_writer_root": (ctypes.c_int, [vp, vp]),
+        "bsg_writer_free": (None, [vp]),
+        "bsg_reader_new": (vp, [vp, vp, ctypes.POINTER(ctypes.c_int)]),
+        "bsg_reader_read": (ctypes.c_int64, [vp, vp, ctypes.c_size_t]),
+        "bsg_reader_seek": (ctypes.c_int64, [vp, ctypes.c_int64, ctypes.c_int]),
+        "bsg_reader_size": (ctypes.c_uint64, [vp]),
+        "bsg_reader_free": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -108,6 +127,13 @@ def lib() -> ctypes.CDLL:
 def _check(rc: int, what: str) -> None:
     if rc != BSG_OK:
         raise BsgError(rc, what)
+
+
+def _as_u8(data) -> np.ndarray:
+    """Zero-copy uint8 view of bytes / bytearray / memoryview / ndarray."""
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data.reshape(-1).view(np.uint8))
+    return np.frombuffer(data, dtype=np.uint8)
 
 
 def _u64(a) -> np.ndarray:
@@ -315,9 +341,9 @@ class StreamingSplitter:
             _check(lib().bsg_set_tile(self.h, tile), "bsg_set_tile")
 
     def write(self, data) -> int:
-        b = bytes(data)
-        _check(lib().bsg_write(self.h, b, len(b)), "bsg_write")
-        return len(b)
+        a = _as_u8(data)
+        _check(lib().bsg_write(self.h, a.ctypes.data, a.nbytes), "bsg_write")
+        return a.nbytes
 
     def close(self) -> None:
         _check(lib().bsg_close(self.h), "bsg_close")
@@ -331,6 +357,141 @@ class StreamingSplitter:
     def free(self) -> None:
         if self.h:
             lib().bsg_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------------------------
+# C++ host mirror (include/bs_split.hpp) through its C ABI: store/mem, split.Writer/Reader.
+# ---------------------------------------------------------------------------------------------
+NOT_FOUND = -2  # bs.ErrNotFound
+
+
+class MemStore:
+    """store/mem (store/mem/mem.go): refs are computed on the GPU."""
+
+    def __init__(self, device: int = 0):
+        self.h = lib().bsg_memstore_new(device)
+        if not self.h:
+            raise BsgError(-12, "bsg_memstore_new")
+
+    def put(self, blob: bytes) -> tuple[bytes, bool]:
+        ref = ctypes.create_string_buffer(32)
+        added = ctypes.c_int(0)
+        b = bytes(blob)
+        _check(lib().bsg_store_put(self.h, b, len(b), ref, ctypes.byref(added)), "put")
+        return ref.raw, bool(added.value)
+
+    def get(self, ref: bytes) -> bytes:
+        n = ctypes.c_size_t(0)
+        rc = lib().bsg_store_get(self.h, bytes(ref), None, 0, ctypes.byref(n))
+        if rc == NOT_FOUND:
+            raise KeyError(bytes(ref).hex())
+        _check(rc, "get")
+        buf = ctypes.create_string_buffer(max(n.value, 1))
+        _check(lib().bsg_store_get(self.h, bytes(ref), buf, n.value, ctypes.byref(n)), "get")
+        return buf.raw[: n.value]
+
+    def refs(self) -> list[bytes]:
+        n = lib().bsg_store_list(self.h, None, 0)
+        buf = ctypes.create_string_buffer(32 * max(n, 1))
+        lib().bsg_store_list(self.h, buf, n)
+        return [buf.raw[32 * i:32 * i + 32] for i in range(n)]
+
+    def __len__(self) -> int:
+        return lib().bsg_store_count(self.h)
+
+    def free(self):
+        if self.h:
+            lib().bsg_store_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Writer:
+    """split.NewWriter(ctx, st, Bits(..), MinSize(..), Fanout(..)) -> Write / Close / Root."""
+
+    def __init__(self, store: MemStore, bits: int = 16, min_size: int = 1024, fanout: int = 8,
+                 device: int = 0, tile: int = 0):
+        err = ctypes.c_int(0)
+        self._p = params(bits, min_size, fanout)
+        self.h = lib().bsg_writer_new(device, store.h, ctypes.byref(self._p), tile,
+                                      ctypes.byref(err))
+        if not self.h:
+            raise BsgError(err.value, "bsg_writer_new")
+        self.store = store
+
+    def write(self, data) -> int:
+        a = _as_u8(data)
+        _check(lib().bsg_writer_write(self.h, a.ctypes.data, a.nbytes), "Write")
+        return a.nbytes
+
+    def close(self) -> None:
+        _check(lib().bsg_writer_close(self.h), "Close")
+
+    @property
+    def root(self) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        _check(lib().bsg_writer_root(self.h, out), "Root")
+        return out.raw
+
+    def free(self):
+        if self.h:
+            lib().bsg_writer_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Reader:
+    """split.NewReader(ctx, g, ref) -> Read / Seek / Size."""
+
+    def __init__(self, store: MemStore, root: bytes):
+        err = ctypes.c_int(0)
+        self.h = lib().bsg_reader_new(store.h, bytes(root), ctypes.byref(err))
+        if not self.h:
+            raise BsgError(err.value, "bsg_reader_new")
+        self.store = store
+
+    def read(self, n: int) -> bytes:
+        buf = ctypes.create_string_buffer(max(n, 1))
+        got = lib().bsg_reader_read(self.h, buf, n)
+        if got < 0:
+            raise BsgError(int(got), "Read")
+        return buf.raw[:got]
+
+    def read_all(self) -> bytes:
+        parts = []
+        while True:
+            b = self.read(1 << 20)
+            if not b:
+                return b"".join(parts)
+            parts.append(b)
+
+    def seek(self, off: int, whence: int = 0) -> int:
+        return lib().bsg_reader_seek(self.h, off, whence)
+
+    @property
+    def size(self) -> int:
+        return lib().bsg_reader_size(self.h)
+
+    def free(self):
+        if self.h:
+            lib().bsg_reader_free(self.h)
             self.h = None
 
     def __del__(self):
