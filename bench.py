@@ -110,6 +110,29 @@ def cpu_baseline(sample_mib: int, bits: int, min_size: int) -> dict | None:
                       f"split+sha256, 1 thread, {len(ch)} chunks in {dt:.2f}s"}
 
 
+KERNEL_NAMES = {"k_scan": "bsg::k_scan(bsg::ScanArgs)", "k_sha": "bsg::k_sha(bsg::ShaArgs)"}
+
+
+def pmc_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary for this workload
+    (profiles/rNN_pmc.json, written by tools/pmc_summary.py from rocprofv3 FETCH_SIZE and
+    WRITE_SIZE passes, gfx950 correction applied there). None if no summary matches."""
+    import glob
+    full = KERNEL_NAMES.get(kernel)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if not workload.startswith(doc.get("workload", "\0")):
+            continue
+        k = doc.get("kernels", {}).get(full)
+        if k:
+            return int(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup()
@@ -167,6 +190,11 @@ def main():
                      and (got["offset"] == ref["offset"]).all())
     cpu = cpu_baseline(args.cpu_sample_mib, args.bits, args.min_size) \
         if (rank == 0 and world == 1) else None
+    workload = ("configs[1]: 1 GiB random stream per GPU, default split params"
+                if (ns == 1 and nbytes == 1 << 30 and args.bits == 16 and args.min_size == 1024)
+                else f"{ns} x {args.stream_mib} MiB streams per GPU")
+    traffic, traffic_src = pmc_traffic(names[dom], workload)
+    scan_gbs = per_launch_bytes / (stage_avg[0] * 1e-3) / 1e9 if stage_avg[0] > 0 else 0.0
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -181,15 +209,18 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic: SplitMix64 counter stream in HBM, seed 0xB5B52026+stream",
-            "config": {"workload": ("configs[1]: 1 GiB random stream per GPU, default split params"
-                                    if (ns == 1 and nbytes == 1 << 30) else
-                                    f"{ns} x {args.stream_mib} MiB streams per GPU"),
+            "config": {"workload": workload,
                        "stream_bytes": nbytes, "streams_per_gpu": ns,
                        "split_bits": args.bits, "min_size": args.min_size, "fanout": 8,
                        "parallelism": "independent streams, one set per GPU, no collectives"},
             "roofline": {"bound": "hbm", "kernel": names[dom],
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_unit": "bytes/launch", "traffic_src": traffic_src,
+                         "algorithmic_bytes": per_launch_bytes,
+                         "limiter": "longest chunk's serial SHA-256 chain (issue latency)",
+                         "k_scan": {"achieved": round(scan_gbs, 1),
+                                    "frac": round(scan_gbs / HBM_PEAK_GBS, 4)}},
             "cpu_baseline": cpu,
             "stage_ms": {n: round(v, 4) for n, v in zip(names, stage_avg)},
             "chunks_per_step": int(chunks),

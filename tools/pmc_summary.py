@@ -1,0 +1,77 @@
+"""Summarise rocprofv3 kernel-trace stats and FETCH_SIZE / WRITE_SIZE passes into profiles/.
+
+Usage: python tools/pmc_summary.py --round r01 [--src gpurun_out]
+
+Reads  <src>/prof_trace/run_kernel_stats.csv            (rocprofv3 --kernel-trace --stats)
+       <src>/prof_fetch/run_counter_collection.csv      (rocprofv3 --pmc FETCH_SIZE)
+       <src>/prof_write/run_counter_collection.csv      (rocprofv3 --pmc WRITE_SIZE)
+Writes profiles/<round>_kernel_stats.csv (verbatim copy) and profiles/<round>_pmc.json:
+  per kernel: launches, FETCH_SIZE / WRITE_SIZE per launch (KiB, raw) and corrected HBM bytes.
+
+Correction (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts
+exactly half the bytes of a wide coalesced streaming read, so FETCH bytes are doubled for the
+kernels whose loads are wide contiguous per-wave reads (k_sha: a wave reads 64 consecutive
+64-byte blocks, 16 B per lane per load). Other kernels keep the raw value and are flagged
+"uncalibrated" (k_scan's loads are 16 B per lane from 64 different 2 KiB strips). WRITE_SIZE is
+exact for the calibrating case (k_fill_splitmix writes 1 GiB and reports 1048576 KiB).
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FETCH_X2 = {"bsg::k_sha(bsg::ShaArgs)", "bsg::k_sha_blobs(bsg::BlobShaArgs)"}
+
+
+def _counters(path):
+    d = collections.defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", required=True)
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--workload", default="configs[1]: 1 GiB random stream per GPU")
+    a = ap.parse_args()
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    stats = os.path.join(a.src, "prof_trace", "run_kernel_stats.csv")
+    shutil.copyfile(stats, os.path.join(out, f"{a.round}_kernel_stats.csv"))
+    avg_ns = {}
+    with open(stats) as f:
+        for r in csv.DictReader(f):
+            avg_ns[r["Name"]] = float(r["AverageNs"])
+    fetch = _counters(os.path.join(a.src, "prof_fetch", "run_counter_collection.csv"))
+    write = _counters(os.path.join(a.src, "prof_write", "run_counter_collection.csv"))
+    kernels = {}
+    for name in sorted(set(fetch) | set(write)):
+        fk = sum(fetch.get(name, [0])) / max(1, len(fetch.get(name, [])))
+        wk = sum(write.get(name, [0])) / max(1, len(write.get(name, [])))
+        x2 = name in FETCH_X2
+        fb = fk * 1024 * (2 if x2 else 1)
+        wb = wk * 1024
+        kernels[name] = {
+            "launches": len(fetch.get(name, [])),
+            "fetch_kib_raw": fk, "write_kib_raw": wk,
+            "fetch_correction": "x2 (wide coalesced reads, gfx950)" if x2 else "uncalibrated (raw)",
+            "hbm_bytes_per_launch": fb + wb,
+            "avg_ns": avg_ns.get(name),
+        }
+    doc = {"round": a.round, "workload": a.workload, "source": "rocprofv3 --pmc FETCH_SIZE / "
+           "WRITE_SIZE, separate passes, bench.py --steps 1 --warmup 0", "kernels": kernels}
+    with open(os.path.join(out, f"{a.round}_pmc.json"), "w") as f:
+        json.dump(doc, f, indent=1)
+    for n, k in kernels.items():
+        if k["hbm_bytes_per_launch"] > 1e6:
+            print(f"{n[:40]:40s} {k['hbm_bytes_per_launch'] / 2**30:8.4f} GiB/launch  avg {k['avg_ns']} ns")
+
+
+if __name__ == "__main__":
+    main()
