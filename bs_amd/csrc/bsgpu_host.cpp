@@ -271,7 +271,7 @@ struct bsg_engine {
     ChunkArgs ca{cand.as<uint64_t>(), flags.as<uint32_t>(), fidx.as<uint64_t>(),
                  bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
                  last_end.as<uint64_t>(), chunk_cap, p, dctr};
-    HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, stream, num_cus)));
+    HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, ns, stream, num_cus)));
 
     ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
                bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),

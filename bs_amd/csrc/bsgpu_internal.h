@@ -11,7 +11,10 @@
 namespace bsg {
 
 constexpr int kScanWG = 512;       // threads per rolling-scan workgroup (8 waves)
-constexpr int kStrip = 2048;       // bytes per lane-strip in the rolling scan
+#ifndef BSG_STRIP
+#define BSG_STRIP 2048
+#endif
+constexpr int kStrip = BSG_STRIP;  // bytes per lane-strip in the rolling scan
 constexpr int kSlotCap = 4;        // candidates kept per strip in the first scan pass
 constexpr int kTabRows = 256;      // buzhash32 table rows
 constexpr int kTabRep = 64;        // one replica per lane: LDS address = byte*256 + lane*4
@@ -92,12 +95,14 @@ struct Counters {
   uint64_t bucket_width;       // LPT bucket width in blocks
   uint64_t diag[5];            // k_sha_long job 0: memtime0/1, realtime0/1, nblocks (diagnostic)
   uint64_t diag2[5];           // k_sha per-lane job order[0]: same fields
-  uint64_t pad_[11];
+  uint64_t rescan;             // strips with more candidates than slots (k_compact re-scans)
+  uint64_t pad_[10];
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 
 constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave-per-chunk path below 64 KiB
 constexpr int kLongRow = 68;               // LDS words per K+W row (64 + pad: conflict-free b128)
+constexpr int kRingWords = 65 * kLongRow;  // per wave: 64 K+W rows + one zero row
 constexpr int kLptBuckets = 4096;          // longest-first job order: counting sort on nblocks
 constexpr uint64_t kReadSlack = 256;       // readable bytes required after every stream's data
 

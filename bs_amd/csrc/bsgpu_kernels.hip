@@ -7,7 +7,7 @@
 //   scan_*      exclusive prefix sums (strip counts -> candidate offsets; flags -> chunk index)
 //   k_compact   slots -> one sorted candidate list (re-scans the rare overflowing strips)
 //   k_select    MinSize greedy as independent walks between "sync points"
-//   k_chunks    boundary list + per-stream counts
+//   k_chunks    boundary list; k_tally per-stream counts
 //   k_sha       batched variable-length SHA-256, one lane per chunk, dynamic per-lane queue
 //
 // Reference semantics being reproduced: hashsplit.Splitter as wired by split.NewWriter
@@ -19,6 +19,13 @@
 #include "bsgpu_internal.h"
 #include "bsgpu_launch.h"
 #include "sha256_device.h"
+
+// Wave-mode round variant: 0 = one lane runs the whole round (14 VALU, default), 1 = lane
+// pairs split it (11 VALU + a DPP exchange; measured slower: the pair's dependent chain per
+// round is longer than the single lane's issue time, tools/ubench/pair.hip).
+#ifndef BSG_PAIR_ROUNDS
+#define BSG_PAIR_ROUNDS 0
+#endif
 
 namespace bsg {
 
@@ -104,9 +111,9 @@ __device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t st
 template <bool WRITE>
 __device__ __forceinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
                                         const uint8_t* d, const StreamDesc* sd, StripCtx& c,
-                                        uint64_t strip, uint64_t off, uint32_t h,
-                                        const uint32_t (&w)[16]) {
-  uint32_t pw[16];
+                                        uint64_t strip, uint64_t off, uint32_t h) {
+  uint32_t w[16], pw[16];
+  load16(d + off, w);
   if (off >= 64) load16(d + off - 64, pw);
   else load16(sd->hist, pw);
   const uint32_t mask = a.p.mask;
@@ -119,8 +126,119 @@ __device__ __forceinline__ void slow_block(const ScanArgs& a, const uint32_t* ta
   }
 }
 
+// k_scan / k_compact allocate no LDS but the dynamic table, so the table starts at LDS
+// address 0 and tab_addr()'s result is the address itself (through the generic pointer the
+// compiler keeps one v_add of the base per lookup). table_at_lds0() guards the assumption; it
+// folds to a constant.
+typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
+__device__ __forceinline__ uint32_t lds_at(const uint32_t*, uint32_t byte_addr) {
+  return *reinterpret_cast<lds_u32p>(static_cast<uintptr_t>(byte_addr));
+}
+__device__ __forceinline__ bool table_at_lds0(const uint32_t* tab) {
+  return (uint32_t)(uintptr_t)((lds_u32p)tab) == 0u;
+}
+
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+// One 64-byte block of the fast loop, software-pipelined: hin[] holds the table values of the
+// previous block (the out-going bytes), hcur[] those of this block (looked up one block
+// earlier). As soon as step k has consumed hin[k], the lookup of byte k of the NEXT block is
+// issued into that register, so ~64 LDS reads are in flight behind the hash chain instead of
+// sitting in front of it, and the two arrays swap roles every block (no register moves).
+// Candidate pre-filter per block:
+//   WIDE (split_bits >= 16): packed min of the low 16 bits of two hashes (v_perm + v_pk_min_u16);
+//   else: min3 of (h & mask).
+// Any block whose pre-filter hits is re-scanned exactly by slow_block().
+template <bool WIDE, bool LOAD>
+__device__ __forceinline__ bool chain64(const uint32_t* tab, const uint32_t (&wnext)[16],
+                                        uint32_t (&hin)[64], const uint32_t (&hcur)[64],
+                                        uint32_t& h, uint32_t lane4, uint32_t mask) {
+  if (WIDE) {
+    u16x2 m = u16x2{0xffff, 0xffff};
+#pragma unroll
+    for (int k = 0; k < 64; k += 2) {
+      const uint32_t h0 = xor3(rotl1(h), hin[k], hcur[k]);
+      h = xor3(rotl1(h0), hin[k + 1], hcur[k + 1]);
+      if (LOAD) {
+        hin[k] = lds_at(tab, tab_addr(wnext[k >> 2], lane4, k));
+        hin[k + 1] = lds_at(tab, tab_addr(wnext[(k + 1) >> 2], lane4, k + 1));
+      }
+      const uint32_t pk = __builtin_amdgcn_perm(h, h0, 0x05040100u);  // lo16(h0) | lo16(h)<<16
+      m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, pk));
+    }
+    return m.x == 0 || m.y == 0;
+  } else {
+    uint32_t m = 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      h = xor3(rotl1(h), hin[k], hcur[k]);
+      if (LOAD) hin[k] = lds_at(tab, tab_addr(wnext[k >> 2], lane4, k));
+      m = min(m, h & mask);
+    }
+    return m == 0;
+  }
+}
+
+__device__ __forceinline__ void lookup64(const uint32_t* tab, const uint32_t (&w)[16],
+                                         uint32_t (&t)[64], uint32_t lane4) {
+#pragma unroll
+  for (int k = 0; k < 64; ++k) t[k] = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
+}
+
+// Fast-loop block loads. BSG_SCAN_NOLOAD (experiment builds only) replaces them with a cheap
+// register pattern to time the loop's compute alone; its results are meaningless.
+__device__ __forceinline__ void scan_load16(const uint8_t* p, uint32_t (&w)[16]) {
+#ifdef BSG_SCAN_NOLOAD
+  const uint32_t x = (uint32_t)(uintptr_t)p * 0x9E3779B1u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = x ^ (0x85EBCA6Bu * (uint32_t)(i + 1));
+#else
+  load16(p, w);
+#endif
+}
+
+// All full 64-byte blocks of a strip. On entry hA = table values of the 64 bytes before the
+// strip and h = the hash there; on exit hA = those of the last full block.
+template <bool WRITE, bool WIDE>
+__device__ __forceinline__ void scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
+                                                 uint32_t lane4, const uint8_t* d,
+                                                 const StreamDesc* sd, StripCtx& c, uint64_t strip,
+                                                 uint32_t nfull, uint32_t& h, uint32_t (&hA)[64]) {
+  const uint32_t mask = a.p.mask;
+  const uint8_t* base = d + c.start;
+  uint32_t hB[64];
+  uint32_t w[16], wn[16];
+  scan_load16(base, w);
+  lookup64(tab, w, hB, lane4);                       // hB = block 0
+  scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
+  uint32_t b = 0;
+  for (; b + 1 < nfull; b += 2) {
+    // block b: out-going hA, in-coming hB; looks up block b+1 into hA
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = wn[i];
+    scan_load16(base + 64ull * min(b + 2, nfull - 1), wn);
+    uint32_t h0 = h;
+    if (__builtin_expect(chain64<WIDE, true>(tab, w, hA, hB, h, lane4, mask), 0))
+      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * b, h0);
+    // block b+1: out-going hB, in-coming hA; looks up block b+2 into hB
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = wn[i];
+    scan_load16(base + 64ull * min(b + 3, nfull - 1), wn);
+    h0 = h;
+    if (__builtin_expect(chain64<WIDE, true>(tab, w, hB, hA, h, lane4, mask), 0))
+      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * (b + 1), h0);
+  }
+  if (b < nfull) {  // odd block count: the last block, then its values back into hA
+    const uint32_t h0 = h;
+    if (__builtin_expect(chain64<WIDE, false>(tab, w, hA, hB, h, lane4, mask), 0))
+      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * b, h0);
+#pragma unroll
+    for (int k = 0; k < 64; ++k) hA[k] = hB[k];
+  }
+}
+
 template <bool WRITE>
-__device__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
+__device__ __forceinline__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
                                uint64_t strip, uint64_t wbase) {
   StripCtx c;
   c.stream = find_stream(a.strip0, a.nstreams, strip);
@@ -141,29 +259,15 @@ __device__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t 
   uint32_t h = 0;
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
-    uint32_t t = lookup(tab, w[k >> 2], lane4, k);
+    uint32_t t = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
     h = rotl1(h) ^ t;
     hist[k] = t;
   }
 
   const uint32_t nfull = len >> 6;
-  if (nfull) load16(d + c.start, w);
-  for (uint32_t b = 0; b < nfull; ++b) {
-    const uint64_t off = c.start + 64ull * b;
-    uint32_t wn[16];
-    load16(d + c.start + 64ull * min(b + 1, nfull - 1), wn);  // prefetch (clamped, branchless)
-    const uint32_t h0 = h;
-    uint32_t m = 0xffffffffu;
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-      uint32_t t = lookup(tab, w[k >> 2], lane4, k);
-      h = xor3(rotl1(h), hist[k], t);
-      hist[k] = t;
-      m = min(m, h & mask);
-    }
-    if (__builtin_expect(m == 0, 0)) slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, off, h0, w);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = wn[i];
+  if (nfull) {
+    if (a.p.split_bits >= 16) scan_full_blocks<WRITE, true>(a, tab, lane4, d, sd, c, strip, nfull, h, hist);
+    else scan_full_blocks<WRITE, false>(a, tab, lane4, d, sd, c, strip, nfull, h, hist);
   }
 
   const uint32_t rem = len & 63u;
@@ -173,7 +277,7 @@ __device__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t 
     for (int k = 0; k < 64; ++k) {
       if ((uint32_t)k < rem) {
         uint32_t byte = d[off + k];
-        uint32_t t = lds_u32(tab, (byte << 8) | lane4);
+        uint32_t t = lds_at(tab, (byte << 8) | lane4);
         h = xor3(rotl1(h), hist[k], t);
         hist[k] = t;
         if ((h & mask) == 0) emit<WRITE>(a, c, strip, off + k, false, tz32(h));
@@ -187,34 +291,43 @@ __device__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t 
   return c.count;
 }
 
-__global__ __launch_bounds__(kScanWG, 4) void k_scan(ScanArgs a) {
+__global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+  if (!table_at_lds0(tab)) {
+    if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
+    return;
+  }
   load_table(tab, a.table);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
-    if (strip < a.nstrips) a.counts[strip] = scan_strip<false>(a, tab, lane4, strip, 0);
+    if (strip < a.nstrips) {
+      const uint32_t n = scan_strip<false>(a, tab, lane4, strip, 0);
+      a.counts[strip] = n;
+      if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
+    }
   }
 }
 
-__global__ __launch_bounds__(kScanWG, 4) void k_compact(ScanArgs a) {
+__global__ __launch_bounds__(kScanWG, 2) void k_compact(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
   if (a.ctr->overflow) return;
-  bool loaded = false;
+  if (!table_at_lds0(tab)) {
+    if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
+    return;
+  }
+  if (a.ctr->rescan) {  // uniform: some strip overflowed its slots, re-scans need the table
+    load_table(tab, a.table);
+    __syncthreads();
+  }
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
     const uint32_t cnt = strip < a.nstrips ? a.counts[strip] : 0u;
-    const bool need = cnt > (uint32_t)kSlotCap;
-    if (__syncthreads_or(need) && !loaded) {
-      load_table(tab, a.table);
-      __syncthreads();
-      loaded = true;
-    }
     if (cnt == 0) continue;
     const uint64_t base = a.cand_off[strip];
-    if (!need) {
+    if (cnt <= (uint32_t)kSlotCap) {
       const uint32_t s = find_stream(a.strip0, a.nstreams, strip);
       const StreamDesc* sd = a.streams + s;
       const uint64_t start = sd->seg_base + (strip - sd->strip0) * (uint64_t)kStrip;
@@ -381,8 +494,31 @@ __global__ __launch_bounds__(256) void k_chunks(ChunkArgs a) {
     }
     a.bnd_end[k] = E;
     a.bnd_info[k] = ((uint64_t)s << 32) | level;
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.scount + s), 1ull);
-    atomicMax(reinterpret_cast<unsigned long long*>(a.last_end + s), (unsigned long long)E);
+  }
+}
+
+// Per-stream chunk count and end of the last chunk. The boundary list is stream-major, so a
+// stream's chunks are one contiguous range found by binary search (no contended atomics: with
+// one stream, 16 K same-address atomics cost ~200 us).
+__device__ __forceinline__ uint64_t first_chunk_of(const uint64_t* info, uint64_t M, uint32_t s) {
+  uint64_t lo = 0, hi = M;  // first k with stream(k) >= s
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint32_t)(info[mid] >> 32) < s) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_tally(ChunkArgs a, uint32_t nstreams) {
+  if (a.ctr->overflow || a.ctr->error) return;
+  const uint64_t M = min(a.ctr->nchunks, a.chunk_cap);
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nstreams;
+       s += gridDim.x * blockDim.x) {
+    const uint64_t lo = first_chunk_of(a.bnd_info, M, s);
+    const uint64_t hi = first_chunk_of(a.bnd_info, M, s + 1);
+    a.scount[s] = hi - lo;
+    if (hi > lo) a.last_end[s] = a.bnd_end[hi - 1];  // else k_init's open_start stays
   }
 }
 
@@ -747,6 +883,12 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t
     tr0 = __builtin_amdgcn_s_memrealtime();
   }
   const uint32_t nblocks = __builtin_amdgcn_readfirstlane(jb.nblocks);
+#if BSG_PAIR_ROUNDS
+  const PairLane pl = pair_lane();
+  uint32_t hs[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hs[k] = pl.odd ? st[k] : st[4 + k];
+#endif
   for (uint32_t base = 0; base < nblocks; base += 64) {
     // phase A: lane i expands block base+i into K+W (LDS row i); lanes past the last block
     // re-expand the last block (their rows are never read) so no load leaves the slack zone
@@ -783,6 +925,11 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t
     ring_sync();
     // phase B: the wave runs the rounds of blocks base .. base+63 uniformly
     const uint32_t nb = min(64u, nblocks - base);
+#if BSG_PAIR_ROUNDS
+    // lane pairs split each round (sha256_rounds_pair); odd lanes read the zero row
+    const uint32_t* zrow = ring + 64 * kLongRow;
+    for (uint32_t i = 0; i < nb; ++i) sha256_rounds_pair(hs, pl.odd ? zrow : ring + i * kLongRow, pl);
+#else
     for (uint32_t i = 0; i < nb; ++i) {
       const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + i * kLongRow);
       uint32_t KW[64];
@@ -793,8 +940,17 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t
       }
       sha256_rounds_kw<true>(st, KW);
     }
+#endif
     ring_sync();
   }
+#if BSG_PAIR_ROUNDS
+  // lane 0 (even: H4..H7) collects H0..H3 from lane 1
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    st[k] = (uint32_t)__builtin_amdgcn_readlane((int)hs[k], 1);
+    st[4 + k] = (uint32_t)__builtin_amdgcn_readlane((int)hs[k], 0);
+  }
+#endif
   if (lane == 0) {
     sha_finish(a, jb, st);
     if (li == 0) {
@@ -836,7 +992,9 @@ __global__ __launch_bounds__(256, 1) void k_sha(ShaArgs a) {
   const uint64_t M = a.ctr->nchunks;
   if (M > a.chunk_cap) return;  // k_chunks flagged the error
   const uint64_t nlong = a.ctr->nlong;
-  uint32_t* ring = lds + (threadIdx.x >> 6) * (64 * kLongRow);
+  uint32_t* ring = lds + (threadIdx.x >> 6) * kRingWords;
+  // zero row after each wave's 64 K+W rows (read by the odd lanes of the paired rounds)
+  for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 0u;
   // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
   // break; }` form was restructured by hipcc into a nested loop that re-entered job 0 forever.
   uint64_t li = pop_uniform(&a.ctr->long_head);
@@ -959,9 +1117,13 @@ hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, i
   return hipGetLastError();
 }
 
-hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus) {
+hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, uint32_t nstreams, hipStream_t s,
+                         int num_cus) {
   const uint32_t grid = grid_for(cand_bound, 256, 8u * (uint32_t)num_cus);
   hipLaunchKernelGGL(k_chunks, dim3(grid), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tally, dim3(grid_for(nstreams, 256, 1024)), dim3(256), 0, s, a, nstreams);
   return hipGetLastError();
 }
 
@@ -971,7 +1133,7 @@ hipError_t launch_init(const InitArgs& a, hipStream_t s) {
 }
 
 constexpr uint32_t kShaLds = 84 * 1024;  // > 80 KiB: one k_sha workgroup per CU (160 KiB LDS)
-static_assert(4 * 64 * kLongRow * 4 <= kShaLds, "wave rings fit");
+static_assert(4 * kRingWords * 4 <= kShaLds, "wave rings fit");
 
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
   (void)job_bound;  // persistent: one workgroup per CU, waves loop over the job queues

@@ -95,7 +95,8 @@ hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus);
 uint64_t prefix_partials_needed(uint64_t n_bound);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s);
 hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);
-hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);
+hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, uint32_t nstreams, hipStream_t s,
+                         int num_cus);
 hipError_t launch_init(const InitArgs& a, hipStream_t s);
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);

@@ -152,4 +152,78 @@ __device__ __forceinline__ void sha256_rounds_kw(uint32_t (&st)[8], const uint32
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Paired-lane rounds for one long chain (wave mode). A single chain is bound by one wave's
+// issue rate (~4.2 cycles per instruction whatever the operands), so what counts is the
+// number of instructions per round. Lane pairs split the round: the even lane holds (e,f,g,h)
+// and computes T1 = h + K+W + Sigma1(e) + Ch(e,f,g); the odd lane holds (a,b,c,d) and computes
+// T2 = Sigma0(a) + Maj(a,b,c). Both run the same 12 instructions (14 for the whole round in
+// one lane):
+//   3 x v_alignbit with per-lane rotate counts, xor3          -> Sigma1 | Sigma0
+//   x = R1 ^ (R3 & xm)   (xm = 0 even, ~0 odd)                -> e     | a^c
+//   F = Ch(x, R2, R3)                                         -> Ch    | Maj  (Maj(a,b,c) = Ch(a^c,b,c))
+//   P = (R4 & pm) + kw   (pm = ~0 even, 0 odd; kw = 0 odd)     -> h+KW  | 0
+//   T = F + S + P                                             -> T1    | T2
+//   Z = odd ? R4 : T ; new = T + Z(partner lane)  (one DPP add) -> d+T1 | T1+T2
+// then (R1..R4) <- (new, R1, R2, R3) by renaming. kw comes from a per-lane LDS row: even lanes
+// read the block's K+W row, odd lanes a row of zeros.
+struct PairLane {
+  uint32_t rot1, rot2, rot3;  // 6,11,25 (even) | 2,13,22 (odd)
+  uint32_t xm, pm;
+  bool odd;
+};
+
+__device__ __forceinline__ PairLane pair_lane() {
+  PairLane p;
+  p.odd = (threadIdx.x & 1u) != 0;
+  p.rot1 = p.odd ? 2u : 6u;
+  p.rot2 = p.odd ? 13u : 11u;
+  p.rot3 = p.odd ? 22u : 25u;
+  p.xm = p.odd ? 0xffffffffu : 0u;
+  p.pm = p.odd ? 0u : 0xffffffffu;
+  return p;
+}
+
+__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
+  // quad_perm [1,0,3,2]: each lane reads its pair partner
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ void pair_round(uint32_t& r1, uint32_t& r2, uint32_t& r3, uint32_t& r4,
+                                           uint32_t kw, const PairLane& p) {
+  const uint32_t S = xor3(rotr(r1, p.rot1), rotr(r1, p.rot2), rotr(r1, p.rot3));
+  const uint32_t x = bitop3<0x78>(r1, r3, p.xm);  // r1 ^ (r3 & xm)
+  const uint32_t F = bitop3<0xCA>(x, r2, r3);
+  const uint32_t P = (r4 & p.pm) + kw;
+  const uint32_t T = F + S + P;
+  const uint32_t Z = p.odd ? r4 : T;
+  const uint32_t n = T + swap_pair(Z);
+  r4 = r3;
+  r3 = r2;
+  r2 = r1;
+  r1 = n;
+}
+
+// 64 rounds on this lane's half state s[4] (even: H4..H7, odd: H0..H3); row = this lane's
+// K+W row (16 x 16 B, zeros on odd lanes). Adds the block result into s.
+__device__ __forceinline__ void sha256_rounds_pair(uint32_t (&s)[4], const uint32_t* row,
+                                                   const PairLane& p) {
+  typedef uint32_t u32x4r __attribute__((ext_vector_type(4), aligned(16)));
+  const u32x4r* r = reinterpret_cast<const u32x4r*>(row);
+  uint32_t r1 = s[0], r2 = s[1], r3 = s[2], r4 = s[3];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const u32x4r kw = r[q];
+    pair_round(r1, r2, r3, r4, kw.x, p);
+    pair_round(r1, r2, r3, r4, kw.y, p);
+    pair_round(r1, r2, r3, r4, kw.z, p);
+    pair_round(r1, r2, r3, r4, kw.w, p);
+  }
+  // after 64 rounds (a multiple of 4) the registers are back in place: r1 = e|a, ...
+  s[0] += r1;
+  s[1] += r2;
+  s[2] += r3;
+  s[3] += r4;
+}
+
 }  // namespace bsg

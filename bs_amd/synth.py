@@ -33,19 +33,26 @@ def splitmix_bytes(seed: int, n: int) -> bytes:
 
 
 def edit_stream(a: np.ndarray, seed: int, sites: int = 1024, span: int = 10486) -> np.ndarray:
-    """Config 5 (dedup): `sites` seeded edits of `span` bytes each (overwrite / insert / delete),
-    applied back to front at uniform positions."""
+    """Config 5 (dedup): stream B = stream A with `sites` seeded edits of `span` bytes each
+    (overwrite / insert / delete, chosen uniformly) at uniform positions of A. Sites are applied
+    in ascending position order; a site that falls inside the previous edit starts right after
+    it. Built with one concatenate (linear in len(a))."""
     rng = np.random.default_rng(seed)
-    pos = np.sort(rng.integers(0, max(len(a) - span, 1), size=sites))[::-1]
+    pos = np.sort(rng.integers(0, max(len(a) - span, 1), size=sites))
     kinds = rng.integers(0, 3, size=sites)
-    out = a
-    for p, k in zip(pos, kinds):
-        p = int(p)
-        fill = rng.integers(0, 256, size=span, dtype=np.uint8)
-        if k == 0:
-            out = np.concatenate([out[:p], fill, out[p + span:]])
-        elif k == 1:
-            out = np.concatenate([out[:p], fill, out[p:]])
-        else:
-            out = np.concatenate([out[:p], out[p + span:]])
-    return out
+    fills = rng.integers(0, 256, size=(sites, span), dtype=np.uint8)
+    parts = []
+    cur = 0
+    for p, k, fill in zip(pos, kinds, fills):
+        p = max(int(p), cur)
+        parts.append(a[cur:p])
+        if k == 0:    # overwrite
+            parts.append(fill)
+            cur = min(p + span, len(a))
+        elif k == 1:  # insert
+            parts.append(fill)
+            cur = p
+        else:         # delete
+            cur = min(p + span, len(a))
+    parts.append(a[cur:])
+    return np.concatenate(parts)

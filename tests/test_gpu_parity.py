@@ -210,3 +210,21 @@ def test_engine_1gib_full_parity(gpu, oracle, table):
     assert int(ch["len"].sum()) == n
     assert (ch["len"][:-1] >= 1024).all()
     eng.close()
+
+
+def test_dedup_edited_streams(gpu, oracle, table):
+    """BASELINE config 5 (dedup), scaled to 2 x 64 MiB: stream B = stream A with 1 % seeded
+    edits (64 sites x 10486 B). Both streams split in one batch must equal the oracle, and the
+    content-defined boundaries must resynchronise after every edit, so most chunks are shared."""
+    from bs_amd.synth import edit_stream, splitmix_array
+    a = splitmix_array(0xB5B52026, 64 << 20)
+    b = edit_stream(a, 0xB5B52026 + 5, sites=64)
+    ch, counts = gpu.split_hash_batch([a, b])
+    na = int(counts[0])
+    for part, data in ((ch[:na], a), (ch[na:], b)):
+        one = oracle.split(table, data)
+        assert as_tuples(part) == as_tuples(one)
+    refs_a = {bytes(r) for r in ch[:na]["ref"]}
+    refs_b = [bytes(r) for r in ch[na:]["ref"]]
+    shared = sum(r in refs_a for r in refs_b) / len(refs_b)
+    assert shared > 0.75, shared

@@ -110,3 +110,17 @@ def test_multistream_oracle_equals_single(oracle, table):
         assert (got["offset"] == one["offset"]).all() and (got["ref"] == one["ref"]).all()
         assert (got["stream"] == i).all()
         k += len(one)
+
+
+def test_edit_stream_boundaries_resynchronise(oracle, table):
+    """Config 5's premise on the oracle (8 MiB, 8 edits): content-defined boundaries realign
+    after each edit, so the chunks of the edited stream are mostly chunks of the original."""
+    from bs_amd.synth import edit_stream, splitmix_array
+    a = splitmix_array(0xB5B52026, 8 << 20)
+    b = edit_stream(a, 0xB5B52026 + 5, sites=8)
+    assert len(b) != len(a) or not np.array_equal(a, b)
+    assert np.array_equal(b, edit_stream(a, 0xB5B52026 + 5, sites=8))  # deterministic
+    ca, cb = oracle.split(table, a), oracle.split(table, b)
+    refs_a = {bytes(r) for r in ca["ref"]}
+    shared = sum(bytes(r) in refs_a for r in cb["ref"]) / len(cb)
+    assert 0.75 < shared < 1.0, shared
