@@ -301,7 +301,7 @@ class Engine:
         d = np.zeros(16, dtype=np.uint64)
         _check(lib().bsg_engine_diag(self.h, _p(d, ctypes.c_uint64)), "bsg_engine_diag")
         out = {"nlong": int(d[0]), "long_thresh": int(d[1]), "max_nblocks": int(d[2]),
-               "nshort": int(d[13])}
+               "nshort": int(d[13]), "wave_tickets": int(d[14]), "total_blocks": int(d[15])}
         for tag, o in (("long", 3), ("lane", 8)):
             cyc, rt, nb = int(d[o + 1] - d[o]), int(d[o + 3] - d[o + 2]), int(d[o + 4])
             if nb and rt:

@@ -201,7 +201,7 @@ struct bsg_engine {
     HCHECK(ctr.ensure(sizeof(Counters)));
     HCHECK(long_list.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(order.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
-    HCHECK(buckets.ensure(sizeof(uint32_t) * 2 * kLptBuckets));
+    HCHECK(buckets.ensure(sizeof(uint32_t) * 4 * kLptBuckets));
     HCHECK(h_streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(h_strip0.ensure(sizeof(uint64_t) * (ns + 1)));
     HCHECK(h_ctr.ensure(sizeof(Counters)));
@@ -214,7 +214,7 @@ struct bsg_engine {
     HCHECK(hipMemcpyAsync(strip0.p, h_strip0.p, sizeof(uint64_t) * (ns + 1),
                           hipMemcpyHostToDevice, stream));
     HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
-    HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * kLptBuckets, stream));
+    HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * 2 * kLptBuckets, stream));
     Counters* dctr = ctr.as<Counters>();
 
     InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
@@ -276,7 +276,9 @@ struct bsg_engine {
     ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
                bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
                carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
-               buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets, long_mode()};
+               buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
+               buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
+               long_mode(), 4u * (uint32_t)num_cus};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
@@ -577,7 +579,8 @@ int bsg_engine_diag(const bsg_engine* e, uint64_t out[16]) {
   for (int i = 0; i < 5; ++i) out[3 + i] = e->last.diag[i];
   for (int i = 0; i < 5; ++i) out[8 + i] = e->last.diag2[i];
   out[13] = e->last.nshort;
-  out[14] = out[15] = 0;
+  out[14] = e->last.ntickets;
+  out[15] = e->last.total_blocks;
   return BSG_OK;
 }
 

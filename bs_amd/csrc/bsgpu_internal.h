@@ -96,13 +96,18 @@ struct Counters {
   uint64_t diag[5];            // k_sha_long job 0: memtime0/1, realtime0/1, nblocks (diagnostic)
   uint64_t diag2[5];           // k_sha per-lane job order[0]: same fields
   uint64_t rescan;             // strips with more candidates than slots (k_compact re-scans)
-  uint64_t pad_[10];
+  uint64_t total_blocks;       // SHA-256 blocks over all jobs (k_lens)
+  uint64_t long_buckets;       // LPT buckets [0, long_buckets) of wave-eligible jobs -> wave mode
+  uint64_t ntickets;           // wave-mode work items: kSolo single jobs, then groups of kGroup
+  uint64_t pad_[7];
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 
-constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave-per-chunk path below 64 KiB
+constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave path below 64 KiB
+constexpr uint32_t kSolo = 8;    // wave mode: the kSolo longest jobs run one per wave,
+constexpr uint32_t kGroup = 8;   // the next ones kGroup per wave (one banked lane pair each)
 constexpr int kLongRow = 68;               // LDS words per K+W row (64 + pad: conflict-free b128)
-constexpr int kRingWords = 65 * kLongRow;  // per wave: 64 K+W rows + one zero row
+constexpr int kRingWords = 65 * kLongRow;  // per wave: 64 K+W rows + one row of ones
 constexpr int kLptBuckets = 4096;          // longest-first job order: counting sort on nblocks
 constexpr uint64_t kReadSlack = 256;       // readable bytes required after every stream's data
 

@@ -20,11 +20,11 @@
 #include "bsgpu_launch.h"
 #include "sha256_device.h"
 
-// Wave-mode round variant: 0 = one lane runs the whole round (14 VALU, default), 1 = lane
-// pairs split it (11 VALU + a DPP exchange; measured slower: the pair's dependent chain per
-// round is longer than the single lane's issue time, tools/ubench/pair.hip).
-#ifndef BSG_PAIR_ROUNDS
-#define BSG_PAIR_ROUNDS 0
+// Wave-mode rounds: 1 (default) = banked lane pair, 10 VALU per round (sha256_rounds_bank,
+// 3180 cycles per block on MI355X); 0 = one lane runs the whole round, 14 VALU (4040 cycles).
+// tools/ubench/pair.hip measures both.
+#ifndef BSG_BANK_ROUNDS
+#define BSG_BANK_ROUNDS 1
 #endif
 
 namespace bsg {
@@ -550,10 +550,6 @@ struct ShaJob {
   uint32_t stream;
 };
 
-__device__ __forceinline__ bool is_long(const ShaJob& jb, uint64_t thresh) {
-  return jb.prefix == 0 && jb.nblocks >= thresh;
-}
-
 __device__ bool sha_setup(const ShaArgs& a, uint64_t j, uint64_t M, ShaJob& jb,
                           uint32_t (&st)[8]) {
   uint32_t s;
@@ -790,48 +786,99 @@ __global__ __launch_bounds__(256) void k_order(ShaArgs a) {
   if (M > a.chunk_cap) return;
   const uint64_t njobs = M + a.nstreams;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t thresh = a.ctr->long_thresh;
+  const uint64_t nlb = a.ctr->long_buckets;  // valid in the SCATTER pass
   uint32_t st[8];
   ShaJob jb;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < njobs; j += stride) {
     if (!sha_setup(a, j, M, jb, st)) continue;
-    if (is_long(jb, thresh)) {
-      if (SCATTER) {
-        const uint64_t k = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->nlong), 1ull);
-        a.long_list[k] = j;
-      }
-      continue;
-    }
     const uint32_t b = lpt_bucket(a.ctr, jb.nblocks);
+    const bool elig = jb.prefix == 0;  // continued chunks (a head from hist) stay per-lane
     if (!SCATTER) {
       atomicAdd(a.bucket_cnt + b, 1u);
+      if (elig) atomicAdd(a.bucket_elig + b, 1u);
+    } else if (elig && b < nlb) {
+      a.long_list[atomicAdd(a.bucket_loff + b, 1u)] = j;
     } else {
-      const uint32_t pos = atomicAdd(a.bucket_off + b, 1u);
-      a.order[pos] = j;
+      a.order[atomicAdd(a.bucket_off + b, 1u)] = j;
     }
   }
 }
 
-__global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
-  // exclusive scan of kLptBuckets counts (4 per thread) -> bucket_off; total -> nshort
-  __shared__ uint32_t wsum[16];
+// Exclusive scan of 4 values per thread over a 1024-thread block; returns the total.
+__device__ __forceinline__ uint32_t block_scan4(uint32_t (&v)[4], uint32_t (&pre)[4],
+                                                uint32_t* wsum) {
   const uint32_t t = threadIdx.x;
-  uint32_t v[4], sum = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { v[i] = a.bucket_cnt[4 * t + i]; sum += v[i]; }
+  const uint32_t sum = v[0] + v[1] + v[2] + v[3];
   uint32_t x = sum;
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = __shfl_up(x, o);
     if ((t & 63) >= (uint32_t)o) x += y;
   }
+  __syncthreads();
   if ((t & 63) == 63) wsum[t >> 6] = x;
   __syncthreads();
-  uint32_t pre = 0;
-  for (uint32_t w = 0; w < (t >> 6); ++w) pre += wsum[w];
-  pre += x - sum;
+  uint32_t p = 0, total = 0;
+  for (uint32_t w = 0; w < 16; ++w) {
+    if (w < (t >> 6)) p += wsum[w];
+    total += wsum[w];
+  }
+  p += x - sum;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { a.bucket_off[4 * t + i] = pre; pre += v[i]; }
-  if (t == 1023) a.ctr->nshort = pre;
+  for (int i = 0; i < 4; ++i) { pre[i] = p; p += v[i]; }
+  return total;
+}
+
+// Splits the jobs between the two SHA-256 paths and lays out both queues, longest first.
+// Bucket b (LPT, b = 0 longest) of wave-eligible jobs goes to wave mode iff its longest
+// length is >= tlen and the wave-mode tickets stay <= half the waves. tlen balances the paths:
+// a per-lane job takes ~2.1x the time per block of a wave-mode one (2.85 vs 1.33-1.42 us), so
+// jobs longer than ~0.42 of the longest would outlast the longest wave-mode job; and no job
+// longer than the per-lane work share (total / lanes) is worth keeping per-lane either.
+__global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t nok;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) nok = 0;
+  const uint64_t mx = a.ctr->max_nblocks, w = a.ctr->bucket_width;
+  uint64_t tlen = (mx * 21) / 50;  // 0.42
+  const uint64_t share = (a.ctr->total_blocks * 9) / (10ull * 64ull * a.waves);
+  tlen = max(max(tlen, share), (uint64_t)kLongMinBlocks);
+  uint64_t cap = kSolo + (uint64_t)kGroup * (a.waves / 2 > kSolo ? a.waves / 2 - kSolo : 0);
+  if (a.long_mode == 2) { tlen = 0; cap = ~0ull; }
+  uint32_t e[4], pe[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = a.bucket_elig[4 * t + i];
+  block_scan4(e, pe, wsum);
+  uint32_t ok = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t b = 4 * t + i;
+    const uint64_t top = mx > b * w ? mx - b * w : 0;  // longest length in bucket b
+    ok += (a.long_mode != 1 && top >= tlen && (uint64_t)pe[i] + e[i] <= cap) ? 1u : 0u;
+  }
+  __syncthreads();
+  atomicAdd(&nok, ok);  // monotone in b: the eligible buckets are a prefix
+  __syncthreads();
+  const uint32_t nlb = nok;
+  uint32_t lv[4], lo[4], sv[4], so[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) lv[i] = (4 * t + i < nlb) ? e[i] : 0u;
+  const uint32_t nlong = block_scan4(lv, lo, wsum);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sv[i] = a.bucket_cnt[4 * t + i] - lv[i];
+  const uint32_t nshort = block_scan4(sv, so, wsum);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a.bucket_loff[4 * t + i] = lo[i];
+    a.bucket_off[4 * t + i] = so[i];
+  }
+  if (t == 0) {
+    a.ctr->long_buckets = nlb;
+    a.ctr->nlong = nlong;
+    a.ctr->nshort = nshort;
+    a.ctr->long_thresh = mx > (uint64_t)nlb * w ? mx - (uint64_t)nlb * w : 0;  // diagnostic
+    a.ctr->ntickets = nlong <= kSolo ? nlong : kSolo + (nlong - kSolo + kGroup - 1) / kGroup;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
@@ -842,23 +889,26 @@ __global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint32_t st[8];
   ShaJob jb;
-  uint64_t mx = 0;
+  uint64_t mx = 0, tot = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < njobs; j += stride)
-    if (sha_setup(a, j, M, jb, st) && jb.prefix == 0) mx = max(mx, (uint64_t)jb.nblocks);
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint64_t)__shfl_down(mx, o));
-  if ((threadIdx.x & 63) == 0 && mx)
-    atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->max_nblocks), (unsigned long long)mx);
+    if (sha_setup(a, j, M, jb, st)) {
+      tot += jb.nblocks;
+      if (jb.prefix == 0) mx = max(mx, (uint64_t)jb.nblocks);
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, (uint64_t)__shfl_down(mx, o));
+    tot += (uint64_t)__shfl_down(tot, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (mx) atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->max_nblocks), (unsigned long long)mx);
+    if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->total_blocks), (unsigned long long)tot);
+  }
 }
 
 __global__ void k_thresh(Counters* ctr, int mode) {
-  // Wave-per-chunk path for jobs >= 60% of the longest: a per-lane wave runs ~1480 VALU per
-  // block against the wave path's ~930, so both paths' longest jobs then end together.
-  const uint64_t t = (ctr->max_nblocks * 3 + 4) / 5;
-  ctr->long_thresh = t > kLongMinBlocks ? t : (uint64_t)kLongMinBlocks;
+  (void)mode;
   const uint64_t w = (ctr->max_nblocks + kLptBuckets) / kLptBuckets;
   ctr->bucket_width = w ? w : 1;
-  if (mode == 1) ctr->long_thresh = ~0ull;  // BSG_LONG_MODE=off: per-lane only
-  if (mode == 2) ctr->long_thresh = 0;      // BSG_LONG_MODE=all: wave mode for everything
 }
 
 // Orders one wave's LDS ring writes before its reads (and reads before the next writes). The
@@ -870,48 +920,76 @@ __device__ __forceinline__ void ring_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Wave mode: the whole wave hashes long job j; ring = this wave's 64 x kLongRow LDS words.
-__device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t j,
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
+// Wave mode: ticket t of the long list (LPT order). Tickets [0, kSolo) are one job each, the
+// rest kGroup consecutive jobs each. The wave expands the message schedule of 64 blocks at a
+// time into its LDS ring (G chains x 64/G blocks; lane l expands block l % B of chain l / B),
+// then each banked lane pair (lanes 8p+3, 8p+4) runs the rounds of its chain, 10 VALU per
+// round (sha256_rounds_bank); a solo job's chain is run by every pair alike.
+__device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t nlong,
                              uint32_t* ring) {
   const uint32_t lane = threadIdx.x & 63u;
+  const bool solo = t < kSolo;
+  const uint64_t j0 = solo ? t : kSolo + (t - kSolo) * kGroup;
+  const uint32_t G = solo ? 1u : kGroup;
+  const uint32_t B = 64u / G;                  // blocks per chain per ring fill
+  const uint32_t cA = lane / B;                // chain this lane expands (phase A)
+  const uint32_t cR = solo ? 0u : lane >> 3;   // chain this lane's pair runs (phase B)
+  // phase-A job
+  ShaJob ja;
+  uint32_t sta[8];
+  const bool va = j0 + cA < nlong && sha_setup(a, a.long_list[j0 + cA], M, ja, sta);
+  if (!va) {  // empty slot of the last group: expand readable bytes, never used
+    ja.dbase = a.data;
+    ja.L = 0;
+    ja.fin = 0;
+    ja.consumed = 0;
+  }
+  const uint32_t na = va ? ja.nblocks : 0u;
+  // phase-B job (also the one this lane's pair finishes)
   ShaJob jb;
   uint32_t st[8];
-  sha_setup(a, j, M, jb, st);
+  const bool vb = j0 + cR < nlong && sha_setup(a, a.long_list[j0 + cR], M, jb, st);
+  const uint32_t nb = vb ? jb.nblocks : 0u;
   uint64_t tm0 = 0, tr0 = 0;
-  if (li == 0) {  // timing stamps of one job (read back as Counters::diag)
+  if (t == 0) {  // timing stamps of the longest job (read back as Counters::diag)
     tm0 = __builtin_amdgcn_s_memtime();
     tr0 = __builtin_amdgcn_s_memrealtime();
   }
-  const uint32_t nblocks = __builtin_amdgcn_readfirstlane(jb.nblocks);
-#if BSG_PAIR_ROUNDS
-  const PairLane pl = pair_lane();
+  const uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
+#if BSG_BANK_ROUNDS
+  const BankLane bl = bank_lane();
   uint32_t hs[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) hs[k] = pl.odd ? st[k] : st[4 + k];
+  for (int k = 0; k < 4; ++k) hs[k] = bl.a_side ? st[k] : st[4 + k];
 #endif
-  for (uint32_t base = 0; base < nblocks; base += 64) {
-    // phase A: lane i expands block base+i into K+W (LDS row i); lanes past the last block
-    // re-expand the last block (their rows are never read) so no load leaves the slack zone
-    const uint32_t blk = min(base + lane, nblocks - 1);
+  for (uint32_t base = 0; base < nmax; base += B) {
+    // phase A: block base + lane % B of chain cA into LDS row `lane`; past a chain's last
+    // block (or for an empty slot) the last block is re-expanded, so no load leaves the slack
+    const uint32_t blk = min(base + lane % B, max(na, 1u) - 1u);
     RawBlock rb;
-    raw_load(jb.dbase, 64ull * blk, 0, jb.L, rb);
+    raw_load(ja.dbase, 64ull * blk, 0, ja.L, rb);
     uint32_t W[16];
     raw_to_words(rb, W);
     if (rb.valid < 64) {
       pad_words(rb.valid, W);
-      if (jb.fin && blk + 1 == jb.nblocks) {
-        const uint64_t bits = (jb.consumed + jb.L) * 8ull;
+      if (ja.fin && blk + 1 == na) {
+        const uint64_t bits = (ja.consumed + ja.L) * 8ull;
         W[14] = (uint32_t)(bits >> 32);
         W[15] = (uint32_t)bits;
       }
     }
     u32x4a* row = reinterpret_cast<u32x4a*>(ring + lane * kLongRow);
 #pragma unroll
-    for (int t = 0; t < 64; t += 4) {
+    for (int tt = 0; tt < 64; tt += 4) {
       uint32_t kw[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int i = t + u;
+        const int i = tt + u;
         if (i >= 16) {
           const uint32_t w15 = W[(i - 15) & 15], w2 = W[(i - 2) & 15];
           const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
@@ -920,40 +998,48 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t
         }
         kw[u] = kK256[i] + W[i & 15];
       }
-      row[t / 4] = u32x4a{kw[0], kw[1], kw[2], kw[3]};
+      row[tt / 4] = u32x4a{kw[0], kw[1], kw[2], kw[3]};
     }
     ring_sync();
-    // phase B: the wave runs the rounds of blocks base .. base+63 uniformly
-    const uint32_t nb = min(64u, nblocks - base);
-#if BSG_PAIR_ROUNDS
-    // lane pairs split each round (sha256_rounds_pair); odd lanes read the zero row
-    const uint32_t* zrow = ring + 64 * kLongRow;
-    for (uint32_t i = 0; i < nb; ++i) sha256_rounds_pair(hs, pl.odd ? zrow : ring + i * kLongRow, pl);
+    // phase B: blocks base .. base+B-1 of every chain
+    const uint32_t steps = min(B, nmax - base);
+#if BSG_BANK_ROUNDS
+    const uint32_t* ones = ring + 64 * kLongRow;
+    for (uint32_t i = 0; i < steps; ++i)
+      sha256_rounds_bank(hs, bl.a_side ? ones : ring + (cR * B + i) * kLongRow, bl,
+                         base + i < nb);
 #else
-    for (uint32_t i = 0; i < nb; ++i) {
-      const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + i * kLongRow);
+    for (uint32_t i = 0; i < steps; ++i) {
+      const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + (cR * B + i) * kLongRow);
       uint32_t KW[64];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const u32x4a v = r[q];
         KW[4 * q] = v.x; KW[4 * q + 1] = v.y; KW[4 * q + 2] = v.z; KW[4 * q + 3] = v.w;
       }
-      sha256_rounds_kw<true>(st, KW);
+      uint32_t s2[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s2[k] = st[k];
+      sha256_rounds_kw<true>(s2, KW);
+      const bool act = base + i < nb;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) st[k] = act ? s2[k] : st[k];
     }
 #endif
     ring_sync();
   }
-#if BSG_PAIR_ROUNDS
-  // lane 0 (even: H4..H7) collects H0..H3 from lane 1
+#if BSG_BANK_ROUNDS
+  // each lane collects its pair's state: H0..H3 from the A lane, H4..H7 from the E lane
+  const int pe = (int)((lane & ~7u) | kBankE), pa = (int)((lane & ~7u) | kBankA);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    st[k] = (uint32_t)__builtin_amdgcn_readlane((int)hs[k], 1);
-    st[4 + k] = (uint32_t)__builtin_amdgcn_readlane((int)hs[k], 0);
+    st[k] = (uint32_t)__shfl((int)hs[k], pa);
+    st[4 + k] = (uint32_t)__shfl((int)hs[k], pe);
   }
 #endif
-  if (lane == 0) {
+  if (vb && (lane & 7u) == 0 && (!solo || lane == 0)) {
     sha_finish(a, jb, st);
-    if (li == 0) {
+    if (t == 0) {
       a.ctr->diag[1] = __builtin_amdgcn_s_memtime();
       a.ctr->diag[3] = __builtin_amdgcn_s_memrealtime();
       a.ctr->diag[0] = tm0;
@@ -963,11 +1049,6 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t li, uint64_t
   }
 }
 
-// The SHA-256 kernel. One 256-thread workgroup per CU (the LDS request admits only one), so
-// each of its 4 waves owns a SIMD: one wave saturates a SIMD's integer VALU (~4.2 cycles per
-// wave-instruction; a second wave on the same SIMD only runs in the first one's gaps), so
-// nothing is gained by stacking waves and the latency-critical wave-mode chains must not
-// share. Every wave first drains the long-job queue in wave mode, then turns per-lane.
 // Wave-uniform queue pop: lane 0 takes the ticket, every lane gets it as an SGPR value.
 __device__ __forceinline__ uint64_t pop_uniform(uint64_t* head) {
   uint32_t lo = 0, hi = 0;
@@ -993,14 +1074,15 @@ __global__ __launch_bounds__(256, 1) void k_sha(ShaArgs a) {
   if (M > a.chunk_cap) return;  // k_chunks flagged the error
   const uint64_t nlong = a.ctr->nlong;
   uint32_t* ring = lds + (threadIdx.x >> 6) * kRingWords;
-  // zero row after each wave's 64 K+W rows (read by the odd lanes of the paired rounds)
-  for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 0u;
+  // row of ones after each wave's 64 K+W rows (the A lanes' kw in sha256_rounds_bank)
+  for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 1u;
   // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
   // break; }` form was restructured by hipcc into a nested loop that re-entered job 0 forever.
-  uint64_t li = pop_uniform(&a.ctr->long_head);
-  while (li < nlong) {
-    sha_wave_job(a, M, li, a.long_list[li], ring);
-    li = pop_uniform(&a.ctr->long_head);
+  const uint64_t ntickets = a.ctr->ntickets;
+  uint64_t t = pop_uniform(&a.ctr->long_head);
+  while (t < ntickets) {
+    sha_wave_job(a, M, t, nlong, ring);
+    t = pop_uniform(&a.ctr->long_head);
   }
   sha_lane_mode(a, M);
 }

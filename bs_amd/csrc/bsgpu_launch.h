@@ -77,9 +77,12 @@ struct ShaArgs {
   uint64_t chunk_cap;
   uint64_t* long_list;      // [chunk_cap + nstreams] job ids for the wave-per-chunk path
   uint64_t* order;          // [chunk_cap + nstreams] per-lane jobs, longest first
-  uint32_t* bucket_cnt;     // [kLptBuckets] zeroed per run
-  uint32_t* bucket_off;     // [kLptBuckets]
+  uint32_t* bucket_cnt;     // [kLptBuckets] all jobs per LPT bucket, zeroed per run
+  uint32_t* bucket_elig;    // [kLptBuckets] wave-eligible jobs per bucket, zeroed per run
+  uint32_t* bucket_off;     // [kLptBuckets] per-lane order offsets
+  uint32_t* bucket_loff;    // [kLptBuckets] long-list offsets
   int long_mode;            // 0 auto, 1 per-lane only, 2 wave mode only (experiments)
+  uint32_t waves;           // waves of the k_sha grid (4 per CU)
 };
 
 struct BlobShaArgs {

@@ -153,77 +153,100 @@ __device__ __forceinline__ void sha256_rounds_kw(uint32_t (&st)[8], const uint32
 }
 
 // ---------------------------------------------------------------------------------------------
-// Paired-lane rounds for one long chain (wave mode). A single chain is bound by one wave's
-// issue rate (~4.2 cycles per instruction whatever the operands), so what counts is the
-// number of instructions per round. Lane pairs split the round: the even lane holds (e,f,g,h)
-// and computes T1 = h + K+W + Sigma1(e) + Ch(e,f,g); the odd lane holds (a,b,c,d) and computes
-// T2 = Sigma0(a) + Maj(a,b,c). Both run the same 12 instructions (14 for the whole round in
-// one lane):
-//   3 x v_alignbit with per-lane rotate counts, xor3          -> Sigma1 | Sigma0
-//   x = R1 ^ (R3 & xm)   (xm = 0 even, ~0 odd)                -> e     | a^c
-//   F = Ch(x, R2, R3)                                         -> Ch    | Maj  (Maj(a,b,c) = Ch(a^c,b,c))
-//   P = (R4 & pm) + kw   (pm = ~0 even, 0 odd; kw = 0 odd)     -> h+KW  | 0
-//   T = F + S + P                                             -> T1    | T2
-//   Z = odd ? R4 : T ; new = T + Z(partner lane)  (one DPP add) -> d+T1 | T1+T2
-// then (R1..R4) <- (new, R1, R2, R3) by renaming. kw comes from a per-lane LDS row: even lanes
-// read the block's K+W row, odd lanes a row of zeros.
-struct PairLane {
-  uint32_t rot1, rot2, rot3;  // 6,11,25 (even) | 2,13,22 (odd)
-  uint32_t xm, pm;
-  bool odd;
+// Banked lane pair for one long chain (wave mode). A single chain is bound by one wave's issue
+// rate (~4.5 cycles per instruction, dependent or not; an s_nop wait state costs the same), so
+// what counts is instructions per round. The round is split over two lanes that run the same
+// 10 instructions (14 for the whole round in one lane), the E lane holding (e,f,g,h) and the
+// A lane (a,b,c,d):
+//   S = Sigma(R1): 3 x v_alignbit with per-lane counts + xor3      E: Sigma1(e)     A: Sigma0(a)
+//   x = R1 ^ (R3 & xm)          (xm = 0 on E, ~0 on A)             E: e             A: a^c
+//   F = Ch(x, R2, R3)                                               E: Ch(e,f,g)     A: Maj(a,b,c)
+//   U = S + F + Q                                                   E: T1 + d = e'   A: T2 - d
+//   n = U + U(lane-1), written on A lanes only (DPP bank mask)     E: e'            A: T1 + T2 = a'
+// with Q prepared during the previous round (in the DPP hazard shadow of U):
+//   P = (R4 ^ xm) + kwl         (kwl = K+W on E, 1 on A)           E: h + KW        A: -d
+//   Q = P + R4(lane+1), written on E lanes only                     E: h + KW + d    A: -d
+// DPP bank masks pick lanes in groups of 4 (bank k of a 16-lane row = lanes 4k..4k+3), so the
+// pair is (lane 3, lane 4) of every 8: E lanes are those with lane & 4 == 0. The other lanes
+// compute garbage and are ignored. kwl comes from a per-lane LDS row (E lanes: the block's K+W
+// row; A lanes: a row of ones).
+struct BankLane {
+  uint32_t rot1, rot2, rot3, xm;
+  bool a_side;
 };
 
-__device__ __forceinline__ PairLane pair_lane() {
-  PairLane p;
-  p.odd = (threadIdx.x & 1u) != 0;
-  p.rot1 = p.odd ? 2u : 6u;
-  p.rot2 = p.odd ? 13u : 11u;
-  p.rot3 = p.odd ? 22u : 25u;
-  p.xm = p.odd ? 0xffffffffu : 0u;
-  p.pm = p.odd ? 0u : 0xffffffffu;
-  return p;
+__device__ __forceinline__ BankLane bank_lane() {
+  BankLane b;
+  b.a_side = (threadIdx.x & 4u) != 0u;
+  b.rot1 = b.a_side ? 2u : 6u;
+  b.rot2 = b.a_side ? 13u : 11u;
+  b.rot3 = b.a_side ? 22u : 25u;
+  b.xm = b.a_side ? 0xffffffffu : 0u;
+  return b;
 }
+constexpr uint32_t kBankE = 3, kBankA = 4;  // the lanes holding (e,f,g,h) and (a,b,c,d)
 
-__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
-  // quad_perm [1,0,3,2]: each lane reads its pair partner
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
-}
-
-__device__ __forceinline__ void pair_round(uint32_t& r1, uint32_t& r2, uint32_t& r3, uint32_t& r4,
-                                           uint32_t kw, const PairLane& p) {
-  const uint32_t S = xor3(rotr(r1, p.rot1), rotr(r1, p.rot2), rotr(r1, p.rot3));
-  const uint32_t x = bitop3<0x78>(r1, r3, p.xm);  // r1 ^ (r3 & xm)
-  const uint32_t F = bitop3<0xCA>(x, r2, r3);
-  const uint32_t P = (r4 & p.pm) + kw;
-  const uint32_t T = F + S + P;
-  const uint32_t Z = p.odd ? r4 : T;
-  const uint32_t n = T + swap_pair(Z);
+// One round, hand-scheduled in one asm block (the compiler's own schedule left the DPP
+// source hazards to s_nop). q in: this round's Q; out: the next round's (from kwn).
+__device__ __forceinline__ void bank_round(uint32_t& r1, uint32_t& r2, uint32_t& r3,
+                                           uint32_t& r4, uint32_t& q, uint32_t kwn,
+                                           const BankLane& b) {
+  uint32_t u, qn, t0, t1, t2, x;
+  asm("v_alignbit_b32 %[t0], %[r1], %[r1], %[s1]\n\t"
+      "v_alignbit_b32 %[t1], %[r1], %[r1], %[s2]\n\t"
+      "v_alignbit_b32 %[t2], %[r1], %[r1], %[s3]\n\t"
+      "v_bitop3_b32 %[x], %[r1], %[r3], %[xm] bitop3:0x78\n\t"
+      "v_bitop3_b32 %[t0], %[t0], %[t1], %[t2] bitop3:0x96\n\t"
+      "v_bitop3_b32 %[x], %[x], %[r2], %[r3] bitop3:0xca\n\t"
+      "v_add3_u32 %[u], %[t0], %[x], %[q]\n\t"
+      "v_xad_u32 %[qn], %[r3], %[xm], %[kwn]\n\t"
+      "v_add_u32_dpp %[qn], %[r3], %[qn] row_shl:1 row_mask:0xf bank_mask:0x5\n\t"
+      "v_add_u32_dpp %[u], %[u], %[u] row_shr:1 row_mask:0xf bank_mask:0xa"
+      : [u] "=&v"(u), [qn] "=&v"(qn), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2),
+        [x] "=&v"(x)
+      : [r1] "v"(r1), [r2] "v"(r2), [r3] "v"(r3), [q] "v"(q), [kwn] "v"(kwn),
+        [s1] "v"(b.rot1), [s2] "v"(b.rot2), [s3] "v"(b.rot3), [xm] "v"(b.xm));
   r4 = r3;
   r3 = r2;
   r2 = r1;
-  r1 = n;
+  r1 = u;
+  q = qn;
 }
 
-// 64 rounds on this lane's half state s[4] (even: H4..H7, odd: H0..H3); row = this lane's
-// K+W row (16 x 16 B, zeros on odd lanes). Adds the block result into s.
-__device__ __forceinline__ void sha256_rounds_pair(uint32_t (&s)[4], const uint32_t* row,
-                                                   const PairLane& p) {
+// Q of round 0 of a block, from the block's starting state.
+__device__ __forceinline__ uint32_t bank_q0(uint32_t r4, uint32_t kw0, const BankLane& b) {
+  uint32_t q;
+  asm("v_xad_u32 %[q], %[r4], %[xm], %[kw]\n\t"
+      "s_nop 1\n\t"
+      "v_add_u32_dpp %[q], %[r4], %[q] row_shl:1 row_mask:0xf bank_mask:0x5"
+      : [q] "=&v"(q)
+      : [r4] "v"(r4), [xm] "v"(b.xm), [kw] "v"(kw0));
+  return q;
+}
+
+// 64 rounds on this lane's half state s[4] (E: H4..H7, A: H0..H3) from this lane's LDS row
+// (16 x 16 B); adds the block result into s if `active` (lanes of finished chains keep theirs).
+__device__ __forceinline__ void sha256_rounds_bank(uint32_t (&s)[4], const uint32_t* row,
+                                                   const BankLane& b, bool active = true) {
   typedef uint32_t u32x4r __attribute__((ext_vector_type(4), aligned(16)));
   const u32x4r* r = reinterpret_cast<const u32x4r*>(row);
   uint32_t r1 = s[0], r2 = s[1], r3 = s[2], r4 = s[3];
+  u32x4r kw = r[0];
+  uint32_t q = bank_q0(r4, kw.x, b);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const u32x4r kw = r[q];
-    pair_round(r1, r2, r3, r4, kw.x, p);
-    pair_round(r1, r2, r3, r4, kw.y, p);
-    pair_round(r1, r2, r3, r4, kw.z, p);
-    pair_round(r1, r2, r3, r4, kw.w, p);
+  for (int i = 0; i < 16; ++i) {
+    const u32x4r kn = r[i < 15 ? i + 1 : 15];
+    bank_round(r1, r2, r3, r4, q, kw.y, b);
+    bank_round(r1, r2, r3, r4, q, kw.z, b);
+    bank_round(r1, r2, r3, r4, q, kw.w, b);
+    bank_round(r1, r2, r3, r4, q, kn.x, b);  // after round 63 this Q is not used
+    kw = kn;
   }
-  // after 64 rounds (a multiple of 4) the registers are back in place: r1 = e|a, ...
-  s[0] += r1;
-  s[1] += r2;
-  s[2] += r3;
-  s[3] += r4;
+  // 64 rounds (a multiple of 4): the names are back in place, r1 = e|a ...
+  s[0] = active ? s[0] + r1 : s[0];
+  s[1] = active ? s[1] + r2 : s[1];
+  s[2] = active ? s[2] + r3 : s[2];
+  s[3] = active ? s[3] + r4 : s[3];
 }
 
 }  // namespace bsg

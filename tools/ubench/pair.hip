@@ -11,6 +11,25 @@ using namespace bsg;
 
 typedef uint32_t u32x4r __attribute__((ext_vector_type(4), aligned(16)));
 
+// Paired lanes (even = E, odd = A) with a cndmask + quad_perm DPP exchange (11 VALU/round).
+struct PairLane {
+  uint32_t rot1, rot2, rot3, xm, pm;
+  bool odd;
+};
+__device__ __forceinline__ PairLane pair_lane() {
+  PairLane p;
+  p.odd = (threadIdx.x & 1u) != 0;
+  p.rot1 = p.odd ? 2u : 6u;
+  p.rot2 = p.odd ? 13u : 11u;
+  p.rot3 = p.odd ? 22u : 25u;
+  p.xm = p.odd ? 0xffffffffu : 0u;
+  p.pm = p.odd ? 0u : 0xffffffffu;
+  return p;
+}
+__device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+}
+
 // V: 0 pair (DPP + cndmask), 1 pair without DPP (wrong values), 2 pair, Z = T (no cndmask),
 //    3 pair with the exchange through ds_swizzle, 4 single-lane rounds_kw
 template <int V>
@@ -37,40 +56,21 @@ __device__ __forceinline__ void round_v(uint32_t& r1, uint32_t& r2, uint32_t& r3
   r4 = r3; r3 = r2; r2 = r1; r1 = n;
 }
 
-// Banked pair: per 8 lanes, lane 3 = E side (e,f,g,h), lane 4 = A side (a,b,c,d); others idle.
-//   P = (R4 ^ xm) + kwl      E: h+KW          A: -d   (xm = ~0, kwl = 1 on A)
-//   Q = P + [E only] R4(lane+1)                E: h+KW+d        A: -d
-//   U = S + F + Q                              E: T1+d = e'     A: T2-d
-//   n = U + [A only] U(lane-1)                 E: e'            A: T2-d+e' = T1+T2 = a'
-struct BankLane {
-  uint32_t rot1, rot2, rot3, xm;
-  bool a_side;
-};
-__device__ __forceinline__ BankLane bank_lane() {
-  BankLane b;
-  b.a_side = (threadIdx.x & 7u) >= 4u;  // lanes 4..7 of each 8 behave as A lanes
-  b.rot1 = b.a_side ? 2u : 6u;
-  b.rot2 = b.a_side ? 13u : 11u;
-  b.rot3 = b.a_side ? 22u : 25u;
-  b.xm = b.a_side ? 0xffffffffu : 0u;
-  return b;
-}
+// Compiler-scheduled version of the banked pair (the header's bank_round is hand-scheduled).
 __device__ __forceinline__ uint32_t xad(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
   asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-__device__ __forceinline__ void bank_round(uint32_t& r1, uint32_t& r2, uint32_t& r3, uint32_t& r4,
-                                           uint32_t kwl, const BankLane& b) {
+__device__ __forceinline__ void bank_round_c(uint32_t& r1, uint32_t& r2, uint32_t& r3, uint32_t& r4,
+                                             uint32_t kwl, const BankLane& b) {
   const uint32_t S = xor3(rotr(r1, b.rot1), rotr(r1, b.rot2), rotr(r1, b.rot3));
   const uint32_t x = bitop3<0x78>(r1, r3, b.xm);
   const uint32_t F = bitop3<0xCA>(x, r2, r3);
   const uint32_t P = xad(r4, b.xm, kwl);
-  // row_shl:1 (0x101): lane i reads lane i+1; bank_mask 0x5 writes banks 0,2 (lanes 0-3, 8-11)
   const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r4, 0x101, 0xF, 0x5, false);
   const uint32_t Q = P + dn;
   const uint32_t U = F + S + Q;
-  // row_shr:1 (0x111): lane i reads lane i-1; bank_mask 0xA writes banks 1,3 (lanes 4-7, 12-15)
   const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)U, 0x111, 0xF, 0xA, false);
   const uint32_t n = U + up;
   r4 = r3; r3 = r2; r2 = r1; r1 = n;
@@ -87,21 +87,36 @@ __global__ void kb(uint64_t* out, uint32_t* io, int blocks) {
   uint32_t s[4], st[8];
   for (int i = 0; i < 4; ++i) s[i] = io[200 + i] + threadIdx.x;
   for (int i = 0; i < 8; ++i) st[i] = io[200 + i] * (uint32_t)(i + 1);
-  if (V == 5)
+  if (V == 5 || V == 6)
     for (int i = 0; i < 4; ++i) s[i] = io[200 + i] * (uint32_t)((bl.a_side ? i : 4 + i) + 1);
   uint64_t t0, t1;
   STAMP(t0);
   for (int b = 0; b < blocks; ++b) {
-    if (V == 5) {
+    if (V == 6) {
+      const u32x4r* r = reinterpret_cast<const u32x4r*>(rows[bl.a_side ? 2 : 0]);
+      uint32_t r1 = s[0], r2 = s[1], r3 = s[2], r4 = s[3];
+      u32x4r kw = r[0];
+      uint32_t q = bank_q0(r4, kw.x, bl);
+#pragma unroll
+      for (int qd = 0; qd < 16; ++qd) {
+        const u32x4r kn = r[qd < 15 ? qd + 1 : 15];
+        bank_round(r1, r2, r3, r4, q, kw.y, bl);
+        bank_round(r1, r2, r3, r4, q, kw.z, bl);
+        bank_round(r1, r2, r3, r4, q, kw.w, bl);
+        bank_round(r1, r2, r3, r4, q, kn.x, bl);  // last round: value unused
+        kw = kn;
+      }
+      s[0] += r1; s[1] += r2; s[2] += r3; s[3] += r4;
+    } else if (V == 5) {
       const u32x4r* r = reinterpret_cast<const u32x4r*>(rows[bl.a_side ? 2 : 0]);
       uint32_t r1 = s[0], r2 = s[1], r3 = s[2], r4 = s[3];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const u32x4r kw = r[q];
-        bank_round(r1, r2, r3, r4, kw.x, bl);
-        bank_round(r1, r2, r3, r4, kw.y, bl);
-        bank_round(r1, r2, r3, r4, kw.z, bl);
-        bank_round(r1, r2, r3, r4, kw.w, bl);
+        bank_round_c(r1, r2, r3, r4, kw.x, bl);
+        bank_round_c(r1, r2, r3, r4, kw.y, bl);
+        bank_round_c(r1, r2, r3, r4, kw.z, bl);
+        bank_round_c(r1, r2, r3, r4, kw.w, bl);
       }
       s[0] += r1; s[1] += r2; s[2] += r3; s[3] += r4;
     } else if (V < 4) {
@@ -136,7 +151,7 @@ __global__ void kb(uint64_t* out, uint32_t* io, int blocks) {
   // final states for the correctness check: single lane (lane 0) vs banked pair (lanes 3, 4)
   if (V == 4 && threadIdx.x == 0)
     for (int i = 0; i < 8; ++i) io[2000 + i] = st[i];
-  if (V == 5 && (threadIdx.x == 3 || threadIdx.x == 4))
+  if ((V == 5 || V == 6) && (threadIdx.x == 3 || threadIdx.x == 4))
     for (int i = 0; i < 4; ++i) io[2000 + (threadIdx.x == 4 ? i : 4 + i)] = s[i];
 }
 
@@ -159,6 +174,7 @@ template <int V> void run(const char* name) {
 int main() {
   run<4>("single lane rounds_kw (14 VALU/round)");
   run<5>("banked pair: xad + 2 masked DPP adds (10 VALU/round)");
+  run<6>("banked pair, hand-scheduled asm round");
   run<0>("pair: cndmask + DPP add (11 VALU/round)");
   run<1>("pair, no DPP (timing only)");
   run<2>("pair, DPP of T, no cndmask (timing only)");
