@@ -20,9 +20,9 @@
 #include "bsgpu_launch.h"
 #include "sha256_device.h"
 
-// Wave-mode rounds: 1 (default) = banked lane pair, 10 VALU per round (sha256_rounds_bank,
-// 3180 cycles per block on MI355X); 0 = one lane runs the whole round, 14 VALU (4040 cycles).
-// tools/ubench/pair.hip measures both.
+// Wave-mode rounds: 1 (default) = skewed lane pairs, 9 VALU per round (sha256_rounds_skew,
+// 2,941 cycles per block on MI355X; the banked pair of sha256_rounds_bank takes 3,161); 0 = one
+// lane runs the whole round, 14 VALU (4,021 cycles). tools/ubench/skew.hip measures all three.
 #ifndef BSG_BANK_ROUNDS
 #define BSG_BANK_ROUNDS 1
 #endif
@@ -831,8 +831,8 @@ __device__ __forceinline__ uint32_t block_scan4(uint32_t (&v)[4], uint32_t (&pre
 // Splits the jobs between the two SHA-256 paths and lays out both queues, longest first.
 // Bucket b (LPT, b = 0 longest) of wave-eligible jobs goes to wave mode iff its longest
 // length is >= tlen and the wave-mode tickets stay <= half the waves. tlen balances the paths:
-// a per-lane job takes ~2.1x the time per block of a wave-mode one (2.85 vs 1.33-1.42 us), so
-// jobs longer than ~0.42 of the longest would outlast the longest wave-mode job; and no job
+// a per-lane job takes ~2.3x the time per block of a wave-mode one (6,820 vs 2,941 cycles), so
+// jobs longer than ~0.43 of the longest would outlast the longest wave-mode job; and no job
 // longer than the per-lane work share (total / lanes) is worth keeping per-lane either.
 __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   __shared__ uint32_t wsum[16];
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   const uint32_t t = threadIdx.x;
   if (t == 0) nok = 0;
   const uint64_t mx = a.ctr->max_nblocks, w = a.ctr->bucket_width;
-  uint64_t tlen = (mx * 21) / 50;  // 0.42
+  uint64_t tlen = (mx * 43) / 100;
   const uint64_t share = (a.ctr->total_blocks * 9) / (10ull * 64ull * a.waves);
   tlen = max(max(tlen, share), (uint64_t)kLongMinBlocks);
   uint64_t cap = kSolo + (uint64_t)kGroup * (a.waves / 2 > kSolo ? a.waves / 2 - kSolo : 0);
@@ -928,8 +928,8 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // Wave mode: ticket t of the long list (LPT order). Tickets [0, kSolo) are one job each, the
 // rest kGroup consecutive jobs each. The wave expands the message schedule of 64 blocks at a
 // time into its LDS ring (G chains x 64/G blocks; lane l expands block l % B of chain l / B),
-// then each banked lane pair (lanes 8p+3, 8p+4) runs the rounds of its chain, 10 VALU per
-// round (sha256_rounds_bank); a solo job's chain is run by every pair alike.
+// then the skewed lane pairs of octet c (lanes 8c+2p: E, 8c+2p+1: A) run the rounds of chain
+// c, 9 VALU per round (sha256_rounds_skew); a solo job's chain is run by every pair alike.
 __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t nlong,
                              uint32_t* ring) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -962,10 +962,13 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   }
   const uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
 #if BSG_BANK_ROUNDS
-  const BankLane bl = bank_lane();
+  // skewed lane pairs (2p: E, 2p+1: A); half states A: H0..H3, E: H6, H7, H4, H5
+  const SkewLane bl = skew_lane();
   uint32_t hs[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) hs[k] = bl.a_side ? st[k] : st[4 + k];
+  hs[0] = bl.a_side ? st[0] : st[6];
+  hs[1] = bl.a_side ? st[1] : st[7];
+  hs[2] = bl.a_side ? st[2] : st[4];
+  hs[3] = bl.a_side ? st[3] : st[5];
 #endif
   for (uint32_t base = 0; base < nmax; base += B) {
     // phase A: block base + lane % B of chain cA into LDS row `lane`; past a chain's last
@@ -1006,7 +1009,7 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
 #if BSG_BANK_ROUNDS
     const uint32_t* ones = ring + 64 * kLongRow;
     for (uint32_t i = 0; i < steps; ++i)
-      sha256_rounds_bank(hs, bl.a_side ? ones : ring + (cR * B + i) * kLongRow, bl,
+      sha256_rounds_skew(hs, bl.a_side ? ones : ring + (cR * B + i) * kLongRow, bl,
                          base + i < nb);
 #else
     for (uint32_t i = 0; i < steps; ++i) {
@@ -1029,13 +1032,14 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     ring_sync();
   }
 #if BSG_BANK_ROUNDS
-  // each lane collects its pair's state: H0..H3 from the A lane, H4..H7 from the E lane
-  const int pe = (int)((lane & ~7u) | kBankE), pa = (int)((lane & ~7u) | kBankA);
+  // each lane collects its octet's first pair: H0..H3 from the A lane, H4..H7 from the E lane
+  const int pe = (int)(lane & ~7u), pa = (int)((lane & ~7u) | 1u);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    st[k] = (uint32_t)__shfl((int)hs[k], pa);
-    st[4 + k] = (uint32_t)__shfl((int)hs[k], pe);
-  }
+  for (int k = 0; k < 4; ++k) st[k] = (uint32_t)__shfl((int)hs[k], pa);
+  st[6] = (uint32_t)__shfl((int)hs[0], pe);
+  st[7] = (uint32_t)__shfl((int)hs[1], pe);
+  st[4] = (uint32_t)__shfl((int)hs[2], pe);
+  st[5] = (uint32_t)__shfl((int)hs[3], pe);
 #endif
   if (vb && (lane & 7u) == 0 && (!solo || lane == 0)) {
     sha_finish(a, jb, st);

@@ -249,4 +249,61 @@ __device__ __forceinline__ void sha256_rounds_bank(uint32_t (&s)[4], const uint3
   s[3] = active ? s[3] + r4 : s[3];
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skewed lane pair (wave mode, default). Same split of the state as the banked pair, but the
+// E lane runs two rounds AHEAD of the A lane, and the two lanes of a pair (2p, 2p+1: E even,
+// A odd) swap one register per round with quad_perm:[1,0,3,2], which needs no bank mask since
+// both lanes keep the DPP result. Register slot V(j) holds e_{j+2} on E lanes and a_j on A
+// lanes; iteration i (R1..R4 = V(i-1)..V(i-4)) computes V(i):
+//   P = (R4 ^ xm) + kwl          E: e_{i-2} + KW_{i+1}          A: -a_{i-4}
+//   Z = P + R2(other lane)       E: h + KW + d of round i+1      A: e_i - a_{i-4} = T1 of round i-1
+//   S = Sigma(R1), F = Ch(R1 ^ (R3 & xm), R2, R3)               E: Sigma1, Ch    A: Sigma0, Maj
+//   V(i) = S + F + Z             E: e_{i+2}                      A: a_i
+// Each lane needs from the other only a value written two iterations earlier, so there is no
+// DPP hazard to wait out: 9 VALU issue slots per round (the banked pair takes 10 + 1 s_nop).
+// A block is iterations -1 .. 64: in -1 and 0 only the E lane's result is kept (the A lane's
+// a_{-1}, a_0 are the chaining values), in 63 and 64 only the A lane's (the E lane keeps e_61,
+// e_62). A lane's half state hs[4] is (H0,H1,H2,H3) on A lanes and (H6,H7,H4,H5) on E lanes, so
+// that the feed-forward hs[k] += V(64-k) is the same instruction on both lanes.
+struct SkewLane {
+  uint32_t rot1, rot2, rot3, xm;
+  bool a_side;
+};
+
+__device__ __forceinline__ SkewLane skew_lane() {
+  SkewLane b;
+  b.a_side = (threadIdx.x & 1u) != 0u;
+  b.rot1 = b.a_side ? 2u : 6u;
+  b.rot2 = b.a_side ? 13u : 11u;
+  b.rot3 = b.a_side ? 22u : 25u;
+  b.xm = b.a_side ? 0xffffffffu : 0u;
+  return b;
+}
+
+// One block (64 rounds) on this lane's half state from its LDS row (E lanes: the block's 64
+// K+W words; A lanes: 64 ones), 16-byte aligned; feed-forward only if `active`. The 66
+// iterations are one generated asm statement (tools/gen_skew_asm.py documents the schedule):
+// as separate asm blocks, each containing the DPP exchange, hipcc put an s_nop in front of
+// every other one.
+#include "sha256_skew_block.inc"
+__device__ __forceinline__ void sha256_rounds_skew(uint32_t (&hs)[4], const uint32_t* row,
+                                                   const SkewLane& b, bool active = true) {
+  // slot s holds V(j), j = s (mod 4): V(-2) = H4|H2, V(-3) = H5|H3, V(-4) = H6|-, V(-5) = H7|H1
+  uint32_t v2 = hs[2], v1 = hs[3], v0 = hs[0], v3 = hs[1];
+  const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const uint32_t*)row);
+  const uint64_t amask = 0xAAAAAAAAAAAAAAAAull;  // A lanes: odd
+  asm volatile(BSG_SKEW_BLOCK_ASM
+               : [v0] "+v"(v0), [v1] "+v"(v1), [v2] "+v"(v2), [v3] "+v"(v3)
+               : [row] "v"(addr), [xm] "v"(b.xm), [s1] "v"(b.rot1), [s2] "v"(b.rot2),
+                 [s3] "v"(b.rot3), [amask] "s"(amask)
+               : "memory", BSG_SKEW_BLOCK_CLOBBERS);
+  if (active) {
+    hs[0] += v0;  // A: a_64 -> H0 | E: e_62 -> H6
+    hs[1] += v3;  // A: a_63 -> H1 | E: e_61 -> H7
+    hs[2] += v2;  // A: a_62 -> H2 | E: e_64 -> H4
+    hs[3] += v1;  // A: a_61 -> H3 | E: e_63 -> H5
+  }
+}
+
 }  // namespace bsg
