@@ -97,6 +97,7 @@ def lib() -> ctypes.CDLL:
         "bsg_memcpy": (ctypes.c_int, [ctypes.c_int, vp, vp, ctypes.c_size_t, ctypes.c_int]),
         "bsg_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
         "bsg_memstore_new": (vp, [ctypes.c_int]),
+        "bsg_filestore_new": (vp, [ctypes.c_char_p, ctypes.c_int]),
         "bsg_store_free": (None, [vp]),
         "bsg_store_count": (ctypes.c_size_t, [vp]),
         "bsg_store_get": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t,
@@ -111,6 +112,7 @@ def lib() -> ctypes.CDLL:
         "bsg_writer_root": (ctypes.c_int, [vp, vp]),
         "bsg_writer_free": (None, [vp]),
         "bsg_reader_new": (vp, [vp, vp, ctypes.POINTER(ctypes.c_int)]),
+        "bsg_reader_open": (vp, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
         "bsg_reader_read": (ctypes.c_int64, [vp, vp, ctypes.c_size_t]),
         "bsg_reader_seek": (ctypes.c_int64, [vp, ctypes.c_int64, ctypes.c_int]),
         "bsg_reader_size": (ctypes.c_uint64, [vp]),
@@ -369,7 +371,10 @@ class StreamingSplitter:
 # ---------------------------------------------------------------------------------------------
 # C++ host mirror (include/bs_split.hpp) through its C ABI: store/mem, split.Writer/Reader.
 # ---------------------------------------------------------------------------------------------
-NOT_FOUND = -2  # bs.ErrNotFound
+NOT_FOUND = -2    # BSG_ENOTFOUND = bs.ErrNotFound
+CORRUPT = -74     # BSG_ECORRUPT: a fetched chunk does not hash to its ref (Reader verify)
+READER_VERIFY = 1
+ERRORS.update({NOT_FOUND: "ENOTFOUND", CORRUPT: "ECORRUPT", -1001: "EIO"})
 
 
 class MemStore:
@@ -418,6 +423,17 @@ class MemStore:
             pass
 
 
+class FileStore(MemStore):
+    """store/file (store/file/file.go): one file per blob at root/blobs/hh/hhhh/<hex>; refs are
+    computed on the GPU (or taken from the split kernels' chunk records by the Writer)."""
+
+    def __init__(self, root: str, device: int = 0):  # noqa: D107 (no MemStore.__init__)
+        self.root = root
+        self.h = lib().bsg_filestore_new(os.fsencode(root), device)
+        if not self.h:
+            raise BsgError(-22, "bsg_filestore_new")
+
+
 class Writer:
     """split.NewWriter(ctx, st, Bits(..), MinSize(..), Fanout(..)) -> Write / Close / Root."""
 
@@ -458,13 +474,15 @@ class Writer:
 
 
 class Reader:
-    """split.NewReader(ctx, g, ref) -> Read / Seek / Size."""
+    """split.NewReader(ctx, g, ref) -> Read / Seek / Size. verify=True checks each leaf node's
+    chunks against their refs with one batched GPU SHA-256 call (BSG_READER_VERIFY)."""
 
-    def __init__(self, store: MemStore, root: bytes):
+    def __init__(self, store: MemStore, root: bytes, verify: bool = False, device: int = 0):
         err = ctypes.c_int(0)
-        self.h = lib().bsg_reader_new(store.h, bytes(root), ctypes.byref(err))
+        self.h = lib().bsg_reader_open(store.h, bytes(root), READER_VERIFY if verify else 0,
+                                       device, ctypes.byref(err))
         if not self.h:
-            raise BsgError(err.value, "bsg_reader_new")
+            raise BsgError(err.value, "bsg_reader_open")
         self.store = store
 
     def read(self, n: int) -> bytes:

@@ -1,0 +1,188 @@
+// bs_filestore.cpp — bs::FileStore, the host mirror of store/file (reference
+// store/file/file.go:20-154): one file per blob at <root>/blobs/<hex[:2]>/<hex[:4]>/<hex>.
+// Put's ref comes from the GPU (GpuHasher -> bsg_sha256_batch) or, through PutWithRef, from the
+// chunk records the split kernels already produced, so an ingest never hashes a blob twice.
+// Anchor-map files (file.go:156-230) are outside the hot path and not mirrored.
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+
+#include "../../include/bs_split.hpp"
+
+namespace bs {
+
+namespace {
+
+Status errno_status(const std::string& what) {
+  return Status::Err(kIO, what + ": " + std::strerror(errno));
+}
+
+// os.MkdirAll(dir, 0755)
+Status mkdir_all(const std::string& dir) {
+  if (dir.empty()) return Status::Ok();
+  struct stat sb;
+  if (::stat(dir.c_str(), &sb) == 0) {
+    if (S_ISDIR(sb.st_mode)) return Status::Ok();
+    errno = ENOTDIR;
+    return errno_status("ensuring path " + dir + " exists");
+  }
+  const size_t slash = dir.find_last_of('/');
+  if (slash != std::string::npos && slash > 0) {
+    Status s = mkdir_all(dir.substr(0, slash));
+    if (!s.ok()) return s;
+  }
+  if (::mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST)
+    return errno_status("ensuring path " + dir + " exists");
+  return Status::Ok();
+}
+
+// ioutil.ReadDir: entries sorted by name, with an is-directory flag; "." and ".." skipped.
+struct Entry {
+  std::string name;
+  bool dir;
+};
+Status read_dir(const std::string& path, std::vector<Entry>* out) {
+  out->clear();
+  DIR* d = ::opendir(path.c_str());
+  if (!d) return errno_status("reading dir " + path);
+  while (struct dirent* e = ::readdir(d)) {
+    const std::string name = e->d_name;
+    if (name == "." || name == "..") continue;
+    bool isdir;
+    if (e->d_type == DT_DIR || e->d_type == DT_REG) {
+      isdir = e->d_type == DT_DIR;
+    } else {  // DT_UNKNOWN on some filesystems
+      struct stat sb;
+      isdir = ::stat((path + "/" + name).c_str(), &sb) == 0 && S_ISDIR(sb.st_mode);
+    }
+    out->push_back({name, isdir});
+  }
+  ::closedir(d);
+  std::sort(out->begin(), out->end(), [](const Entry& a, const Entry& b) { return a.name < b.name; });
+  return Status::Ok();
+}
+
+bool is_hex(const std::string& s) {
+  return !s.empty() && std::all_of(s.begin(), s.end(), [](char c) {
+    return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+  });
+}
+
+}  // namespace
+
+bool RefFromHex(const std::string& hex, Ref* out) {
+  if (hex.size() != 64 || !is_hex(hex)) return false;
+  auto nib = [](char c) -> int {
+    return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10;
+  };
+  for (int i = 0; i < 32; ++i) (*out)[i] = (uint8_t)(nib(hex[2 * i]) << 4 | nib(hex[2 * i + 1]));
+  return true;
+}
+
+std::string FileStore::BlobPath(const Ref& ref) const {  // file.go:33-40
+  const std::string h = RefString(ref);
+  return root_ + "/blobs/" + h.substr(0, 2) + "/" + h.substr(0, 4) + "/" + h;
+}
+
+Status FileStore::Get(const Ref& ref, std::vector<uint8_t>* out) {  // file.go:42-50
+  const std::string path = BlobPath(ref);
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) {
+    if (errno == ENOENT) return Status::Err(kNotFound, "not found");
+    return errno_status("opening " + path);
+  }
+  out->clear();
+  struct stat sb;
+  if (::fstat(fd, &sb) == 0 && sb.st_size > 0) out->reserve((size_t)sb.st_size);
+  uint8_t buf[1 << 16];
+  for (;;) {
+    const ssize_t k = ::read(fd, buf, sizeof buf);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      Status s = errno_status("opening " + path);
+      ::close(fd);
+      return s;
+    }
+    if (k == 0) break;
+    out->insert(out->end(), buf, buf + k);
+  }
+  ::close(fd);
+  return Status::Ok();
+}
+
+Status FileStore::Put(const uint8_t* data, size_t n, Ref* ref, bool* added) {  // file.go:52-76
+  Ref r;
+  Status s = hasher_.Sum(data, n, &r);
+  if (!s.ok()) return s;
+  if (ref) *ref = r;
+  return PutWithRef(r, data, n, added);
+}
+
+Status FileStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) {
+  if (added) *added = false;
+  const std::string path = BlobPath(ref);
+  Status s = mkdir_all(path.substr(0, path.find_last_of('/')));
+  if (!s.ok()) return s;
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0644);
+  if (fd < 0) {
+    if (errno == EEXIST) return Status::Ok();  // already present: (ref, false, nil)
+    return errno_status("creating " + path);
+  }
+  size_t done = 0;
+  while (done < n) {
+    const ssize_t k = ::write(fd, data + done, n - done);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      s = errno_status("writing data to " + path);
+      ::close(fd);
+      return s;
+    }
+    done += (size_t)k;
+  }
+  if (::close(fd) != 0) return errno_status("writing data to " + path);
+  if (added) *added = true;
+  return Status::Ok();
+}
+
+// file.go:79-154: walk blobs/<2>/<4>/<64> in name order, starting after `start`.
+Status FileStore::ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) {
+  const std::string blobroot = root_ + "/blobs";
+  Status s = mkdir_all(blobroot);
+  if (!s.ok()) return s;
+  std::vector<Entry> top, mid, blobs;
+  s = read_dir(blobroot, &top);
+  if (!s.ok()) return s;
+  const std::string sh = RefString(start);
+  auto ti = std::lower_bound(top.begin(), top.end(), sh.substr(0, 2),
+                             [](const Entry& e, const std::string& k) { return e.name < k; });
+  for (; ti != top.end(); ++ti) {
+    if (!ti->dir || ti->name.size() != 2 || !is_hex(ti->name)) continue;
+    const std::string tdir = blobroot + "/" + ti->name;
+    s = read_dir(tdir, &mid);
+    if (!s.ok()) return s;
+    auto mi = std::lower_bound(mid.begin(), mid.end(), sh.substr(0, 4),
+                               [](const Entry& e, const std::string& k) { return e.name < k; });
+    for (; mi != mid.end(); ++mi) {
+      if (!mi->dir || mi->name.size() != 4 || !is_hex(mi->name)) continue;
+      s = read_dir(tdir + "/" + mi->name, &blobs);
+      if (!s.ok()) return s;
+      auto bi = std::upper_bound(blobs.begin(), blobs.end(), sh,
+                                 [](const std::string& k, const Entry& e) { return k < e.name; });
+      for (; bi != blobs.end(); ++bi) {
+        if (bi->dir) continue;
+        Ref r;
+        if (!RefFromHex(bi->name, &r)) continue;
+        s = f(r);
+        if (!s.ok()) return s;
+      }
+    }
+  }
+  return Status::Ok();
+}
+
+}  // namespace bs

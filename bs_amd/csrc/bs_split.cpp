@@ -376,7 +376,8 @@ Status get_node(Store* g, const Ref& ref, Node* n) {
 }
 }  // namespace
 
-std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err) {
+std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err, bool verify,
+                                    int device) {
   Status dummy;
   if (!err) err = &dummy;
   Node n;
@@ -387,9 +388,38 @@ std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err) {
   }
   std::unique_ptr<Reader> r(new Reader());
   r->g_ = g;
+  r->verify_ = verify;
+  r->device_ = device;
   r->stack_.push_back(std::move(n));
   *err = Status::Ok();
   return r;
+}
+
+// Verify mode: one batched GPU SHA-256 over all chunks of the current leaf node.
+Status Reader::LoadLeaves() {
+  const std::vector<Child>& leaves = stack_.back().leaves;
+  cache_.assign(leaves.size(), {});
+  std::vector<uint64_t> off(leaves.size()), len(leaves.size());
+  uint64_t total = 0;
+  for (size_t k = 0; k < leaves.size(); ++k) {
+    Status s = g_->Get(leaves[k].ref, &cache_[k]);
+    if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
+    off[k] = total;
+    len[k] = cache_[k].size();
+    total += len[k];
+  }
+  std::vector<uint8_t> packed(total ? total : 1);
+  for (size_t k = 0; k < leaves.size(); ++k)
+    if (len[k]) std::memcpy(packed.data() + off[k], cache_[k].data(), len[k]);
+  std::vector<uint8_t> refs(32 * leaves.size());
+  int rc = bsg_sha256_batch(device_, packed.data(), off.data(), len.data(),
+                            (uint32_t)leaves.size(), refs.data());
+  if (rc) return Status::Err(rc, std::string("verifying chunks: ") + bsg_errstr(rc));
+  for (size_t k = 0; k < leaves.size(); ++k)
+    if (std::memcmp(refs.data() + 32 * k, leaves[k].ref.data(), 32) != 0)
+      return Status::Err(kCorrupt, "chunk " + RefString(leaves[k].ref) + " fails verification");
+  cache_valid_ = true;
+  return Status::Ok();
 }
 
 Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
@@ -404,6 +434,7 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
         return Status::Ok();
       }
       stack_.pop_back();
+      cache_valid_ = false;
     }
     for (;;) {  // descend to the leaf node
       const Node& node = stack_.back();
@@ -419,14 +450,22 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
       Status s = get_node(g_, node.nodes[index].ref, &child);
       if (!s.ok()) return Status::Err(s.code, "getting tree node: " + s.msg);
       stack_.push_back(std::move(child));
+      cache_valid_ = false;
+    }
+    if (verify_ && !cache_valid_) {
+      Status s = LoadLeaves();
+      if (!s.ok()) return s;
     }
     const std::vector<Child>& leaves = stack_.back().leaves;
     size_t k = 0;
     while (leaves.size() - k > 1 && leaves[k + 1].offset <= pos_) ++k;
     for (; k < leaves.size() && len > 0; ++k) {
-      std::vector<uint8_t> chunk;
-      Status s = g_->Get(leaves[k].ref, &chunk);
-      if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
+      std::vector<uint8_t> fetched;
+      if (!verify_) {
+        Status s = g_->Get(leaves[k].ref, &fetched);
+        if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
+      }
+      const std::vector<uint8_t>& chunk = verify_ ? cache_[k] : fetched;
       const uint64_t skip = pos_ - leaves[k].offset;
       const size_t avail = chunk.size() - (size_t)skip;
       const size_t take = std::min(avail, len);
@@ -458,8 +497,8 @@ uint64_t Reader::Seek(int64_t offset, int whence) {
 // C ABI wrappers (bsgpu.h) so the Python tests can drive the C++ host mirror.
 // ---------------------------------------------------------------------------------------------
 struct bsg_store {
-  bs::MemStore mem;
-  explicit bsg_store(int device) : mem(device) {}
+  std::unique_ptr<bs::Store> st;
+  bs::MemStore* mem = nullptr;  // set for store/mem (O(1) count)
 };
 struct bsg_writer {
   std::unique_ptr<bs::split::Writer> w;
@@ -470,16 +509,43 @@ struct bsg_reader {
 
 extern "C" {
 
-bsg_store* bsg_memstore_new(int device) { return new (std::nothrow) bsg_store(device); }
+bsg_store* bsg_memstore_new(int device) {
+  bsg_store* s = new (std::nothrow) bsg_store();
+  if (!s) return nullptr;
+  s->mem = new (std::nothrow) bs::MemStore(device);
+  s->st.reset(s->mem);
+  if (!s->mem) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+bsg_store* bsg_filestore_new(const char* root, int device) {
+  if (!root || !*root) return nullptr;
+  bsg_store* s = new (std::nothrow) bsg_store();
+  if (!s) return nullptr;
+  s->st.reset(new (std::nothrow) bs::FileStore(root, device));
+  if (!s->st) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
 void bsg_store_free(bsg_store* s) { delete s; }
-size_t bsg_store_count(const bsg_store* s) { return s ? s->mem.Size() : 0; }
+size_t bsg_store_count(const bsg_store* s) {
+  if (!s) return 0;
+  if (s->mem) return s->mem->Size();
+  size_t k = 0;
+  s->st->ListRefs(bs::Zero, [&](const bs::Ref&) { ++k; return bs::Status::Ok(); });
+  return k;
+}
 
 int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n) {
   if (!s || !ref || !n) return BSG_EINVAL;
   bs::Ref r;
   std::memcpy(r.data(), ref, 32);
   std::vector<uint8_t> b;
-  bs::Status st = s->mem.Get(r, &b);
+  bs::Status st = s->st->Get(r, &b);
   if (!st.ok()) return st.code;
   *n = b.size();
   if (out) std::memcpy(out, b.data(), std::min(cap, b.size()));
@@ -490,7 +556,7 @@ int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[3
   if (!s || (!data && n)) return BSG_EINVAL;
   bs::Ref r;
   bool a = false;
-  bs::Status st = s->mem.Put(data, n, &r, &a);
+  bs::Status st = s->st->Put(data, n, &r, &a);
   if (!st.ok()) return st.code;
   if (ref_out) std::memcpy(ref_out, r.data(), 32);
   if (added) *added = a ? 1 : 0;
@@ -500,7 +566,7 @@ int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[3
 size_t bsg_store_list(bsg_store* s, uint8_t* refs, size_t cap) {
   if (!s) return 0;
   size_t k = 0;
-  s->mem.ListRefs(bs::Zero, [&](const bs::Ref& r) {
+  s->st->ListRefs(bs::Zero, [&](const bs::Ref& r) {
     if (k < cap && refs) std::memcpy(refs + 32 * k, r.data(), 32);
     ++k;
     return bs::Status::Ok();
@@ -525,7 +591,7 @@ bsg_writer* bsg_writer_new(int device, bsg_store* s, const bsg_params* params, s
   o.device = device;
   o.tile = tile;
   bs::Status st;
-  auto w = bs::split::Writer::New(&s->mem, o, &st);
+  auto w = bs::split::Writer::New(s->st.get(), o, &st);
   if (!w) {
     *err = st.code;
     return nullptr;
@@ -547,6 +613,11 @@ int bsg_writer_root(const bsg_writer* w, uint8_t out[32]) {
 void bsg_writer_free(bsg_writer* w) { delete w; }
 
 bsg_reader* bsg_reader_new(bsg_store* s, const uint8_t root[32], int* err) {
+  return bsg_reader_open(s, root, 0, 0, err);
+}
+
+bsg_reader* bsg_reader_open(bsg_store* s, const uint8_t root[32], int flags, int device,
+                            int* err) {
   int dummy;
   if (!err) err = &dummy;
   if (!s || !root) {
@@ -556,7 +627,7 @@ bsg_reader* bsg_reader_new(bsg_store* s, const uint8_t root[32], int* err) {
   bs::Ref r;
   std::memcpy(r.data(), root, 32);
   bs::Status st;
-  auto rd = bs::split::Reader::New(&s->mem, r, &st);
+  auto rd = bs::split::Reader::New(s->st.get(), r, &st, (flags & BSG_READER_VERIFY) != 0, device);
   if (!rd) {
     *err = st.code;
     return nullptr;

@@ -7,6 +7,8 @@
 //   bs::RefPutter (optional, like MultiPutter store.go:44-47): Put with a ref the caller already
 //                 computed on the GPU, so a backend need not hash the blob again
 //   bs::MemStore                           store/mem/mem.go:17-124
+//   bs::FileStore                          store/file/file.go:20-154 (blob layout and ListRefs;
+//                                          anchors are out of scope)
 //   bs::split::Writer  New/Write/Close/Root, options Bits/MinSize/Fanout   split/split.go:30-165
 //   bs::split::Reader  New/Read/Seek/Size                                  split/split.go:173-303
 //   bs::split::Node / Child (proto3 wire format)                           split/split.proto:6-26
@@ -39,7 +41,9 @@ struct Status {
   static Status Ok() { return Status{}; }
   static Status Err(int c, std::string m) { return Status{c, std::move(m)}; }
 };
-constexpr int kNotFound = -2;  // bs.ErrNotFound (store.go:63)
+constexpr int kNotFound = BSG_ENOTFOUND;  // bs.ErrNotFound (store.go:63)
+constexpr int kCorrupt = BSG_ECORRUPT;    // a fetched blob does not hash to its ref (Reader verify)
+constexpr int kIO = BSG_EIO;              // filesystem error (errno text in Status::msg)
 
 class Store {
  public:
@@ -82,6 +86,27 @@ class MemStore : public Store, public RefPutter {
   std::map<Ref, std::vector<uint8_t>> blobs_;
   GpuHasher hasher_;
 };
+
+// store/file: blobs live at <root>/blobs/<hex[:2]>/<hex[:4]>/<hex> (file.go:33-40). Put hashes
+// on the GPU and creates the file with O_CREAT|O_EXCL (an existing file means "already
+// present", file.go:52-76); PutWithRef skips the hash when the caller has the GPU's ref.
+class FileStore : public Store, public RefPutter {
+ public:
+  explicit FileStore(std::string root, int device = 0)
+      : root_(std::move(root)), hasher_(device) {}
+  Status Get(const Ref& ref, std::vector<uint8_t>* out) override;
+  Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) override;
+  Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
+  Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
+  std::string BlobPath(const Ref& ref) const;
+  const std::string& Root() const { return root_; }
+
+ private:
+  std::string root_;
+  GpuHasher hasher_;
+};
+
+bool RefFromHex(const std::string& hex, Ref* out);  // bs.RefFromHex (bs.go)
 
 namespace split {
 
@@ -145,8 +170,11 @@ class Writer {
 
 class Reader {
  public:
-  // split.NewReader(ctx, g, ref)
-  static std::unique_ptr<Reader> New(Store* g, const Ref& root, Status* err);
+  // split.NewReader(ctx, g, ref). verify (not in the reference, which trusts its store): the
+  // leaves of each leaf node are fetched together and their SHA-256 checked against their refs
+  // in one batched GPU call (bsg_sha256_batch); a mismatch fails the Read with kCorrupt.
+  static std::unique_ptr<Reader> New(Store* g, const Ref& root, Status* err,
+                                     bool verify = false, int device = 0);
   // io.Reader: returns bytes read; 0 with *eof = true at the end.
   Status Read(uint8_t* buf, size_t n, size_t* got, bool* eof);
   // io.Seeker (whence: 0 start, 1 current, 2 end).
@@ -155,9 +183,14 @@ class Reader {
 
  private:
   Reader() = default;
+  Status LoadLeaves();  // verify mode: fetch + check every leaf of stack_.back()
   Store* g_ = nullptr;
   uint64_t pos_ = 0;
   std::vector<Node> stack_;  // stack_[0] is the root
+  bool verify_ = false;
+  int device_ = 0;
+  bool cache_valid_ = false;                 // cache_ holds stack_.back()'s leaves
+  std::vector<std::vector<uint8_t>> cache_;  // verified chunks of that leaf node
 };
 
 }  // namespace split

@@ -39,6 +39,9 @@ extern "C" {
 #define BSG_EDEVICE (-5)   /* HIP runtime / kernel error */
 #define BSG_ESTATE (-71)   /* Write after Close, etc. */
 #define BSG_ENODEV (-19)   /* no such HIP device */
+#define BSG_ENOTFOUND (-2) /* bs.ErrNotFound (store.go:63) */
+#define BSG_ECORRUPT (-74) /* a fetched blob does not hash to its ref (reader verify) */
+#define BSG_EIO (-1001)    /* filesystem error (store/file) */
 
 /* split.Writer options. Zero fields take hashsplit's own defaults (SplitBits 13, MinSize 64);
  * bsg_params_default() gives split.NewWriter's defaults (16 / 1024 / fanout 8,
@@ -141,11 +144,13 @@ int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed
 
 /* ---- C++ host mirror of split.Writer / split.Reader / store/mem (bs_split.hpp), exposed for
  * C callers and tests ---- */
-typedef struct bsg_store bsg_store;   /* store/mem (store/mem/mem.go:17-124); refs via GPU */
-bsg_store* bsg_memstore_new(int device);
+typedef struct bsg_store bsg_store;   /* a bs.Store; every Put's ref comes from the GPU */
+bsg_store* bsg_memstore_new(int device);   /* store/mem  (store/mem/mem.go:17-124) */
+/* store/file (store/file/file.go:20-154): blobs at <root>/blobs/<hex[:2]>/<hex[:4]>/<hex>. */
+bsg_store* bsg_filestore_new(const char* root, int device);
 void bsg_store_free(bsg_store* s);
 size_t bsg_store_count(const bsg_store* s);
-/* Get: copies min(cap, len) bytes, *n = blob length; returns kNotFound (-2) if absent. */
+/* Get: copies min(cap, len) bytes, *n = blob length; returns BSG_ENOTFOUND if absent. */
 int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n);
 int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[32], int* added);
 /* All refs in lexicographic order (32 bytes each, up to cap); returns the total count. */
@@ -161,6 +166,11 @@ void bsg_writer_free(bsg_writer* w);
 
 typedef struct bsg_reader bsg_reader; /* split.NewReader / Read / Seek / Size */
 bsg_reader* bsg_reader_new(bsg_store* s, const uint8_t root[32], int* err);
+/* flags: BSG_READER_VERIFY = check every fetched chunk's SHA-256 against its ref, one batched
+ * GPU call per leaf node (a mismatch fails the read with BSG_ECORRUPT). */
+#define BSG_READER_VERIFY 1
+bsg_reader* bsg_reader_open(bsg_store* s, const uint8_t root[32], int flags, int device,
+                            int* err);
 int64_t bsg_reader_read(bsg_reader* r, uint8_t* buf, size_t n); /* bytes; 0 at EOF; <0 error */
 int64_t bsg_reader_seek(bsg_reader* r, int64_t off, int whence);
 uint64_t bsg_reader_size(const bsg_reader* r);
