@@ -72,7 +72,9 @@ def lib() -> ctypes.CDLL:
         "bsg_pending": (ctypes.c_size_t, [vp]),
         "bsg_drain": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
         "bsg_set_tile": (ctypes.c_int, [vp, ctypes.c_size_t]),
+        "bsg_set_carry_cap": (ctypes.c_int, [vp, ctypes.c_size_t]),
         "bsg_free": (None, [vp]),
+        "bsg_reset": (ctypes.c_int, [vp]),
         "bsg_engine_create": (vp, [ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_int)]),
         "bsg_engine_destroy": (None, [vp]),
         "bsg_engine_run": (ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint32,
@@ -332,7 +334,7 @@ class StreamingSplitter:
     """bsg_open/bsg_write/bsg_close/bsg_drain: the C-ABI form of split.Writer's chunking."""
 
     def __init__(self, bits: int = 16, min_size: int = 1024, fanout: int = 8, table=None,
-                 device: int = 0, tile: int | None = None):
+                 device: int = 0, tile: int | None = None, carry_cap: int | None = None):
         err = ctypes.c_int(0)
         self._p = params(bits, min_size, fanout)
         self._t, tp = _table_arg(table)
@@ -341,6 +343,8 @@ class StreamingSplitter:
             raise BsgError(err.value, "bsg_open")
         if tile is not None:
             _check(lib().bsg_set_tile(self.h, tile), "bsg_set_tile")
+        if carry_cap is not None:
+            _check(lib().bsg_set_carry_cap(self.h, carry_cap), "bsg_set_carry_cap")
 
     def write(self, data) -> int:
         a = _as_u8(data)
@@ -349,6 +353,9 @@ class StreamingSplitter:
 
     def close(self) -> None:
         _check(lib().bsg_close(self.h), "bsg_close")
+
+    def reset(self) -> None:
+        _check(lib().bsg_reset(self.h), "bsg_reset")
 
     def drain(self) -> np.ndarray:
         n = lib().bsg_pending(self.h)

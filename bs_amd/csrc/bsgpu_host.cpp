@@ -15,6 +15,7 @@
 #include <cstring>
 #include <deque>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/bsgpu.h"
@@ -140,6 +141,11 @@ struct bsg_engine {
   DevBuf table, streams, strip0, counts, slots, strip_off, partials_a, partials_b, cand, flags,
       fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets;
   PinBuf h_streams, h_strip0, h_ctr;
+  // Optional snapshot right after selection (streaming pipeline): the counters and every
+  // stream's last chunk end land in pinned memory and sel_ev fires, long before k_sha ends.
+  bool snapshot = false;
+  PinBuf h_snap;  // Counters, then nstreams x u64 last_end
+  hipEvent_t sel_ev = nullptr;
   // current run
   const uint8_t* d_data = nullptr;
   std::vector<StreamDesc> descs;
@@ -272,6 +278,15 @@ struct bsg_engine {
                  bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
                  last_end.as<uint64_t>(), chunk_cap, p, dctr};
     HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, ns, stream, num_cus)));
+    if (snapshot) {
+      HCHECK(h_snap.ensure(sizeof(Counters) + 8ull * (ns ? ns : 1)));
+      if (!sel_ev) HCHECK(hipEventCreateWithFlags(&sel_ev, hipEventDisableTiming));
+      HCHECK(hipMemcpyAsync(h_snap.p, ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+      if (ns)
+        HCHECK(hipMemcpyAsync(static_cast<uint8_t*>(h_snap.p) + sizeof(Counters), last_end.p,
+                              8ull * ns, hipMemcpyDeviceToHost, stream));
+      HCHECK(hipEventRecord(sel_ev, stream));
+    }
 
     ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
                bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
@@ -319,63 +334,255 @@ struct bsg_engine {
   }
 };
 
-struct bsg_ctx {
+// ------------------------------------------------------------------------------------------
+// Streaming split.Writer (bsg_open / bsg_write / bsg_close / bsg_drain): a pipeline of kSlots
+// tiles, each with its own engine (HIP stream + work buffers), device slot and pinned staging.
+//
+//   host:  copy Write()s into staging[i] ... submit tile i ... copy into staging[i+1] ...
+//   slot:  [carry area kCarryCap | tile bytes | read slack]
+//   GPU :  H2D(i) -> scan/select(i) -> sel_ev(i) -> k_sha(i) -> D2H records(i)
+//
+// Tile i+1 needs from tile i only where its open chunk starts, which is known at sel_ev(i), a
+// fraction of a millisecond into tile i: the open chunk's bytes (at most kCarryCap; k_sha
+// leaves such a chunk unhashed) are copied device-to-device in front of tile i+1's bytes and
+// hashed there from the start. Tile i's k_sha — bound by its longest chunk's serial SHA-256
+// chain — therefore runs concurrently with tiles i+1, i+2, ... instead of in front of them.
+// A longer open chunk falls back to the midstate carry: tile i hashes its whole blocks, and
+// tile i+1 waits for tile i's k_sha and continues from the exported midstate.
+// Records complete in tile order; bsg_pending/bsg_drain hand them out in stream order.
+// ------------------------------------------------------------------------------------------
+constexpr int kMaxSlots = 8;
+constexpr uint64_t kDefaultCarryCap = 8ull << 20;
+// Tiles in flight. Each has its own HIP stream, and streams beyond the process's hardware
+// queues (GPU_MAX_HW_QUEUES, 4 by default) share a queue and serialise behind each other's
+// k_sha, so the default stays below that.
+int default_slots() {
+  const char* e = std::getenv("BSG_STREAM_SLOTS");
+  const int v = e ? std::atoi(e) : 3;
+  return std::max(2, std::min(kMaxSlots, v));
+}
+
+struct TileSlot {
   bsg_engine* eng = nullptr;
+  DevBuf dbuf;            // carry area + tile + slack
+  PinBuf staging;         // this tile's host bytes
+  PinBuf recs;            // records, D2H'd after k_sha
+  hipEvent_t h2d_ev = nullptr, done_ev = nullptr;
+  // state of the tile currently using the slot
+  bool busy = false;          // submitted, records not yet collected
+  bool sel_read = false;      // selection snapshot consumed (open_next / nchunks known)
+  bool recs_enq = false;      // D2H of records enqueued (done_ev recorded)
+  bool final_seg = false;
+  uint64_t seg_base = 0, len = 0, nchunks = 0, open_next = 0;
+};
+
+struct bsg_ctx {
   bsg_params params{};
   Params p{};
+  int dev = 0;
   size_t tile = 256ull << 20;
-  PinBuf staging;
-  DevBuf dtile;
+  uint64_t carry_cap = kDefaultCarryCap;
+  int nslots = default_slots();
+  TileSlot slots[kMaxSlots];
+  int cur = 0;              // slot the host is filling
   size_t fill = 0;
-  uint64_t pos = 0;         // stream bytes already handed to the device
-  uint64_t open_start = 0;  // open chunk start (stream offset)
-  uint64_t consumed = 0;    // open chunk bytes folded into mid
-  uint32_t prefix_len = 0;  // open chunk bytes not yet hashed (the tail of hist)
-  uint32_t mid[8];
-  uint8_t hist[64];
+  int prev = -1;            // last submitted slot (its open chunk continues into `cur`)
+  std::deque<int> inflight; // submitted slots in stream order
+  uint64_t pos = 0;         // stream offset of slots[cur]'s first byte
+  uint8_t hist[64];         // the 64 stream bytes before pos
   std::deque<bsg_chunk> ready;
-  std::vector<bsg_chunk> tmp;
-  bool closed = false;
+  bool closed = false, started = false;
   int sticky = BSG_OK;
 
-  int process(bool final_seg) {
-    if (fill == 0 && !final_seg) return BSG_OK;
-    HCHECK(dtile.ensure(fill + kReadSlack));
-    if (fill) HCHECK(hipMemcpyAsync(dtile.p, staging.p, fill, hipMemcpyHostToDevice, eng->stream));
+  int init(int device, const uint32_t* table) {
+    dev = device;
+    for (int k = 0; k < nslots; ++k) {
+      TileSlot& t = slots[k];
+      int err = BSG_OK;
+      t.eng = bsg_engine_create(device, table, &err);
+      if (!t.eng) return err;
+      t.eng->snapshot = true;
+      HCHECK(hipEventCreateWithFlags(&t.h2d_ev, hipEventDisableTiming));
+      HCHECK(hipEventCreateWithFlags(&t.done_ev, hipEventDisableTiming));
+    }
+    std::memset(hist, 0, 64);
+    return BSG_OK;
+  }
+
+  void release() {
+    hipSetDevice(dev);
+    for (TileSlot& t : slots) {
+      if (t.eng) hipStreamSynchronize(t.eng->stream);
+      t.dbuf.release();
+      t.staging.release();
+      t.recs.release();
+      if (t.h2d_ev) hipEventDestroy(t.h2d_ev);
+      if (t.done_ev) hipEventDestroy(t.done_ev);
+      bsg_engine_destroy(t.eng);
+      t.eng = nullptr;
+    }
+  }
+
+  // Selection of slot i is done: learn its chunk count and where its open chunk starts. A
+  // candidate-buffer overflow (degenerate input) is re-run synchronously at exact capacity.
+  int read_sel(int i) {
+    TileSlot& t = slots[i];
+    if (t.sel_read) return BSG_OK;
+    HCHECK(hipEventSynchronize(t.eng->sel_ev));
+    Counters c = *t.eng->h_snap.as<Counters>();
+    uint64_t last_end =
+        *reinterpret_cast<const uint64_t*>(t.eng->h_snap.as<uint8_t>() + sizeof(Counters));
+    if (c.overflow || c.error) {
+      uint64_t n = 0;
+      int rc = t.eng->finish(&n);  // synchronous; re-runs after an overflow
+      if (rc) return rc;
+      c = t.eng->last;
+      HCHECK(hipMemcpy(&last_end, t.eng->last_end.p, 8, hipMemcpyDeviceToHost));
+    }
+    t.nchunks = c.nchunks;
+    t.open_next = last_end;
+    t.sel_read = true;
+    return BSG_OK;
+  }
+
+  // Enqueue the D2H of slot i's records behind its k_sha.
+  int enqueue_recs(int i) {
+    TileSlot& t = slots[i];
+    if (t.recs_enq) return BSG_OK;
+    int rc = read_sel(i);
+    if (rc) return rc;
+    HCHECK(t.recs.ensure(sizeof(bsg_chunk) * (t.nchunks ? t.nchunks : 1)));
+    if (t.nchunks)
+      HCHECK(hipMemcpyAsync(t.recs.p, t.eng->out.p, sizeof(bsg_chunk) * t.nchunks,
+                            hipMemcpyDeviceToHost, t.eng->stream));
+    HCHECK(hipMemcpyAsync(t.eng->h_ctr.p, t.eng->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost,
+                          t.eng->stream));
+    HCHECK(hipEventRecord(t.done_ev, t.eng->stream));
+    t.recs_enq = true;
+    return BSG_OK;
+  }
+
+  // Wait for the oldest in-flight tile (if `wait`) and move its records to `ready`.
+  int collect_front(bool wait, bool* got) {
+    *got = false;
+    if (inflight.empty()) return BSG_OK;
+    const int i = inflight.front();
+    TileSlot& t = slots[i];
+    if (!t.recs_enq) {
+      if (!wait) return BSG_OK;
+      int rc = enqueue_recs(i);
+      if (rc) return rc;
+    }
+    if (!wait) {
+      hipError_t q = hipEventQuery(t.done_ev);
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return BSG_OK;
+      }
+      HCHECK(q);
+    }
+    HCHECK(hipEventSynchronize(t.done_ev));
+    const Counters& c = *t.eng->h_ctr.as<Counters>();
+    if (c.error) {
+      std::fprintf(stderr, "bsgpu: device sanity check failed (code %llu)\n",
+                   (unsigned long long)c.error);
+      return BSG_EDEVICE;
+    }
+    const bsg_chunk* r = t.recs.as<bsg_chunk>();
+    for (uint64_t k = 0; k < t.nchunks; ++k) ready.push_back(r[k]);
+    t.busy = false;
+    t.eng->enqueued = false;
+    inflight.pop_front();
+    *got = true;
+    return BSG_OK;
+  }
+
+  int poll() {
+    bool got = true;
+    while (got) {
+      int rc = collect_front(false, &got);
+      if (rc) return rc;
+    }
+    return BSG_OK;
+  }
+
+  // Make slots[i] free for a new tile: its previous tile's records are collected.
+  int reclaim(int i) {
+    while (slots[i].busy) {
+      bool got = false;
+      int rc = collect_front(true, &got);
+      if (rc) return rc;
+    }
+    return BSG_OK;
+  }
+
+  int submit(bool final_seg) {
+    const int i = cur;
+    TileSlot& t = slots[i];
+    bsg_engine* e = t.eng;
+    HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
+    uint8_t* base = t.dbuf.as<uint8_t>();
     StreamDesc d{};
-    d.data_off = 0;
+    d.data_off = carry_cap;
     d.len = fill;
     d.seg_base = pos;
-    d.open_start = open_start;
-    d.consumed = consumed;
     d.finalize = final_seg ? 1u : 0u;
-    d.prefix_len = prefix_len;
-    std::memcpy(d.mid, mid, sizeof mid);
+    d.carry_cap = final_seg ? 0u : (uint32_t)std::min<uint64_t>(carry_cap, 0xffffffffu);
     std::memcpy(d.hist, hist, 64);
-    eng->d_data = dtile.as<uint8_t>();
-    eng->descs.assign(1, d);
-    eng->nstreams = 1;
-    eng->p = p;
-    int rc = eng->enqueue();
-    if (rc) return rc;
-    uint64_t n = 0;
-    rc = eng->finish(&n);
-    if (rc) return rc;
-    tmp.resize(n);
-    if (n)
-      HCHECK(hipMemcpy(tmp.data(), eng->out.p, sizeof(bsg_chunk) * n, hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < n; ++i) ready.push_back(tmp[i]);
-    if (!final_seg) {
-      CarryOut co;
-      HCHECK(hipMemcpy(&co, eng->carry.p, sizeof co, hipMemcpyDeviceToHost));
-      if (!co.valid) return BSG_EDEVICE;
-      open_start = co.open_start;
-      consumed = co.consumed;
-      prefix_len = co.prefix_len;
-      std::memcpy(mid, co.mid, sizeof mid);
+    std::memcpy(d.mid, kIV, sizeof kIV);
+    if (prev >= 0) {
+      TileSlot& pt = slots[prev];
+      int rc = read_sel(prev);
+      if (rc) return rc;
+      const uint64_t open = pt.open_next;
+      const uint64_t carry = pos - open;
+      d.open_start = open;
+      if (carry <= pt.eng->descs[0].carry_cap) {  // bytes carried on the device
+        if (carry) {
+          // the open chunk may itself have started in front of pt's tile (carried into it)
+          const uint8_t* src =
+              pt.dbuf.as<uint8_t>() + (int64_t)carry_cap + ((int64_t)open - (int64_t)pt.seg_base);
+          HCHECK(hipMemcpyAsync(base + carry_cap - carry, src, carry, hipMemcpyDeviceToDevice,
+                                e->stream));
+          // the previous slot must not be overwritten before this copy has read it
+          HCHECK(hipEventRecord(t.h2d_ev, e->stream));
+          HCHECK(hipStreamWaitEvent(pt.eng->stream, t.h2d_ev, 0));
+          d.flags = kDescOpenInDevice;
+        }
+      } else {  // midstate carry: wait for the previous tile's k_sha
+        rc = enqueue_recs(prev);
+        if (rc) return rc;
+        HCHECK(hipEventSynchronize(pt.done_ev));
+        CarryOut co;
+        HCHECK(hipMemcpy(&co, pt.eng->carry.p, sizeof co, hipMemcpyDeviceToHost));
+        if (!co.valid || co.open_start != open) return BSG_EDEVICE;
+        d.consumed = co.consumed;
+        d.prefix_len = co.prefix_len;
+        std::memcpy(d.mid, co.mid, sizeof co.mid);
+      }
+      // the previous tile's records can be fetched as soon as its k_sha is done
+      rc = enqueue_recs(prev);
+      if (rc) return rc;
     }
-    // window history = last 64 bytes of the stream so far
-    const uint8_t* seg = staging.as<uint8_t>();
+    if (fill)
+      HCHECK(hipMemcpyAsync(base + carry_cap, t.staging.p, fill, hipMemcpyHostToDevice,
+                            e->stream));
+    HCHECK(hipEventRecord(t.h2d_ev, e->stream));
+    e->d_data = base;
+    e->descs.assign(1, d);
+    e->nstreams = 1;
+    e->p = p;
+    int rc = e->enqueue();
+    if (rc) return rc;
+    t.busy = true;
+    t.sel_read = false;
+    t.recs_enq = false;
+    t.final_seg = final_seg;
+    t.seg_base = pos;
+    t.len = fill;
+    inflight.push_back(i);
+    // window history for the next tile = the last 64 stream bytes so far
+    const uint8_t* seg = t.staging.as<uint8_t>();
     if (fill >= 64) {
       std::memcpy(hist, seg + fill - 64, 64);
     } else if (fill) {
@@ -384,6 +591,89 @@ struct bsg_ctx {
     }
     pos += fill;
     fill = 0;
+    prev = i;
+    cur = (cur + 1) % nslots;
+    if (final_seg) return enqueue_recs(i);
+    return BSG_OK;
+  }
+
+  // Host side of Write: bytes into the current slot's pinned staging (large pieces on several
+  // threads), submitting full tiles as more data arrives.
+  int write(const uint8_t* p, size_t n) {
+    while (n) {
+      if (fill == tile) {  // full tile and more data coming: submit it (never the last one)
+        int rc = submit(false);
+        if (rc) return rc;
+      }
+      TileSlot& t = slots[cur];
+      if (fill == 0) {
+        int rc = reclaim(cur);
+        if (rc) return rc;
+        HCHECK(t.staging.ensure(tile));
+        HCHECK(hipEventSynchronize(t.h2d_ev));  // staging free once its H2D has run
+      }
+      const size_t k = std::min(n, tile - fill);
+      par_copy(t.staging.as<uint8_t>() + fill, p, k);
+      fill += k;
+      p += k;
+      n -= k;
+    }
+    return poll();
+  }
+
+  static void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    constexpr size_t kPiece = 2ull << 20;  // per thread, at least
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned nt = (unsigned)std::min<size_t>({(size_t)8, (size_t)hw, n / kPiece});
+    if (nt <= 1) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + nt - 1) / nt;
+    for (unsigned k = 0; k < nt; ++k) {
+      const size_t o = k * per;
+      if (o >= n) break;
+      th.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(per, n - o)); });
+    }
+    for (auto& x : th) x.join();
+  }
+
+  // Start a new stream on the same buffers (bsg_reset): everything in flight is finished first.
+  int reset() {
+    while (!inflight.empty()) {
+      bool got = false;
+      int rc = collect_front(true, &got);
+      if (rc) return rc;
+    }
+    ready.clear();
+    cur = 0;
+    fill = 0;
+    prev = -1;
+    pos = 0;
+    std::memset(hist, 0, 64);
+    closed = false;
+    started = false;
+    sticky = BSG_OK;
+    return BSG_OK;
+  }
+
+  int close() {
+    if (fill == 0 && pos == 0) return BSG_OK;  // empty stream: no chunks
+    // (a stream that ends exactly at a tile boundary flushes its open chunk with an empty
+    // final segment)
+    int rc = reclaim(cur);
+    if (rc) return rc;
+    if (fill == 0) {
+      HCHECK(slots[cur].staging.ensure(16));
+    }
+    rc = submit(true);
+    if (rc) return rc;
+    while (!inflight.empty()) {
+      bool got = false;
+      rc = collect_front(true, &got);
+      if (rc) return rc;
+    }
     return BSG_OK;
   }
 };
@@ -473,6 +763,8 @@ void bsg_engine_destroy(bsg_engine* e) {
   e->h_streams.release();
   e->h_strip0.release();
   e->h_ctr.release();
+  e->h_snap.release();
+  if (e->sel_ev) hipEventDestroy(e->sel_ev);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }
@@ -594,26 +886,36 @@ bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, i
     *err = rc;
     return nullptr;
   }
-  bsg_engine* e = bsg_engine_create(device, table, err);
-  if (!e) return nullptr;
+  if (device < 0 || device >= bsg_device_count()) {
+    *err = BSG_ENODEV;
+    return nullptr;
+  }
   bsg_ctx* c = new (std::nothrow) bsg_ctx();
   if (!c) {
-    bsg_engine_destroy(e);
     *err = BSG_ENOMEM;
     return nullptr;
   }
-  c->eng = e;
   c->params = norm;
   c->p = p;
-  std::memcpy(c->mid, kIV, sizeof kIV);
-  std::memset(c->hist, 0, 64);
+  if (hipSetDevice(device) != hipSuccess || (rc = c->init(device, table)) != BSG_OK) {
+    c->release();
+    delete c;
+    *err = rc ? rc : BSG_EDEVICE;
+    return nullptr;
+  }
   *err = BSG_OK;
   return c;
 }
 
 int bsg_set_tile(bsg_ctx* c, size_t tile) {
-  if (!c || tile < 4096 || c->fill || c->pos) return BSG_EINVAL;
+  if (!c || tile < 4096 || c->fill || c->pos || c->started) return BSG_EINVAL;
   c->tile = tile;
+  return BSG_OK;
+}
+
+int bsg_set_carry_cap(bsg_ctx* c, size_t bytes) {
+  if (!c || c->fill || c->pos || c->started || bytes > 0xffffffffull) return BSG_EINVAL;
+  c->carry_cap = bytes;
   return BSG_OK;
 }
 
@@ -622,21 +924,11 @@ int bsg_write(bsg_ctx* c, const uint8_t* p, size_t n) {
   if (c->closed) return BSG_ESTATE;
   if (c->sticky) return c->sticky;
   if (n && !p) return BSG_EINVAL;
-  int rc = c->eng->setdev();
-  if (rc) return rc;
-  if (n) HCHECK(c->staging.ensure(c->tile));
-  while (n) {
-    if (c->fill == c->tile) {  // full tile and more data coming: process it (never the last)
-      rc = c->process(false);
-      if (rc) return c->sticky = rc;
-    }
-    const size_t k = std::min(n, c->tile - c->fill);
-    std::memcpy(c->staging.as<uint8_t>() + c->fill, p, k);
-    c->fill += k;
-    p += k;
-    n -= k;
-  }
-  return BSG_OK;
+  if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
+  c->started = true;
+  int rc = c->write(p, n);
+  if (rc) c->sticky = rc;
+  return rc;
 }
 
 int bsg_close(bsg_ctx* c) {
@@ -644,18 +936,28 @@ int bsg_close(bsg_ctx* c) {
   if (c->closed) return c->sticky;
   c->closed = true;
   if (c->sticky) return c->sticky;
-  int rc = c->eng->setdev();
-  if (rc) return c->sticky = rc;
-  if (c->fill == 0 && c->pos == 0) return BSG_OK;  // empty stream: no chunks
-  rc = c->process(true);
+  if (hipSetDevice(c->dev) != hipSuccess) return c->sticky = BSG_EDEVICE;
+  int rc = c->close();
   if (rc) c->sticky = rc;
   return rc;
 }
 
-size_t bsg_pending(const bsg_ctx* c) { return c ? c->ready.size() : 0; }
+size_t bsg_pending(const bsg_ctx* c) {
+  if (!c) return 0;
+  bsg_ctx* m = const_cast<bsg_ctx*>(c);  // polling completed tiles is not a visible change
+  if (!m->sticky && hipSetDevice(m->dev) == hipSuccess) {
+    int rc = m->poll();
+    if (rc) m->sticky = rc;
+  }
+  return m->ready.size();
+}
 
 size_t bsg_drain(bsg_ctx* c, bsg_chunk* out, size_t cap) {
   if (!c || !out) return 0;
+  if (!c->sticky && hipSetDevice(c->dev) == hipSuccess) {
+    int rc = c->poll();
+    if (rc) c->sticky = rc;
+  }
   size_t k = 0;
   while (k < cap && !c->ready.empty()) {
     out[k++] = c->ready.front();
@@ -664,15 +966,15 @@ size_t bsg_drain(bsg_ctx* c, bsg_chunk* out, size_t cap) {
   return k;
 }
 
+int bsg_reset(bsg_ctx* c) {
+  if (!c) return BSG_EINVAL;
+  if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
+  return c->reset();
+}
+
 void bsg_free(bsg_ctx* c) {
   if (!c) return;
-  if (c->eng) {
-    hipSetDevice(c->eng->dev);
-    hipStreamSynchronize(c->eng->stream);
-  }
-  c->staging.release();
-  c->dtile.release();
-  bsg_engine_destroy(c->eng);
+  c->release();
   delete c;
 }
 

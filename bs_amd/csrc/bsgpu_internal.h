@@ -51,9 +51,13 @@ struct StreamDesc {            // 160 bytes, 16-byte aligned
   uint32_t finalize;           // 1: flush the tail as the final chunk (Splitter.Close)
   uint32_t prefix_len;         // open-chunk bytes held in hist[64-prefix_len..63], < 64
   uint32_t mid[8];             // SHA-256 midstate of the open chunk (IV when consumed == 0)
-  uint32_t pad_[2];
+  uint32_t carry_cap;          // non-final segment: leave an open chunk of <= carry_cap bytes
+                               // unhashed (the next segment re-hashes it from device memory)
+  uint32_t flags;              // kDescOpenInDevice: the open chunk's bytes [open_start, seg_base)
+                               // sit in device memory right before data_off (consumed == 0)
   uint8_t hist[64];            // the 64 stream bytes before seg_base (zeros before offset 0)
 };
+constexpr uint32_t kDescOpenInDevice = 1;
 static_assert(sizeof(StreamDesc) == 160, "StreamDesc layout");
 
 struct CarryOut {              // open chunk state after a non-final segment

@@ -568,14 +568,17 @@ __device__ bool sha_setup(const ShaArgs& a, uint64_t j, uint64_t M, ShaJob& jb,
     if (sd->finalize) return false;
     jb.start = a.last_end[s];
     jb.end = sd->seg_base + sd->len;
+    // a short open chunk is carried to the next segment as bytes, not as a midstate
+    if (jb.end - jb.start <= sd->carry_cap) return false;
     jb.level = 0;
     jb.fin = 0;
   }
   const StreamDesc* sd = a.streams + s;
   jb.id = j;
   jb.stream = s;
-  uint64_t dstart;
-  if (jb.start < sd->seg_base) {  // continues the open chunk of the previous segment
+  int64_t dstart;  // negative: the open chunk's head precedes the segment in device memory
+  if (jb.start < sd->seg_base && !(sd->flags & kDescOpenInDevice)) {
+    // continues the open chunk of the previous segment from its midstate
     jb.prefix = sd->prefix_len;
     jb.consumed = sd->consumed;
 #pragma unroll
@@ -586,15 +589,15 @@ __device__ bool sha_setup(const ShaArgs& a, uint64_t j, uint64_t M, ShaJob& jb,
     jb.consumed = 0;
     st[0] = 0x6a09e667; st[1] = 0xbb67ae85; st[2] = 0x3c6ef372; st[3] = 0xa54ff53a;
     st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
-    dstart = jb.start - sd->seg_base;
+    dstart = (int64_t)jb.start - (int64_t)sd->seg_base;
   }
-  jb.dbase = a.data + sd->data_off + dstart;
+  jb.dbase = a.data + (int64_t)sd->data_off + dstart;
   jb.hist = sd->hist + 64 - jb.prefix;
   if (jb.end < jb.start || jb.end > sd->seg_base + sd->len || jb.start < sd->open_start) {
     atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);  // bug guard
     return false;
   }
-  jb.L = jb.prefix + (jb.end - sd->seg_base - dstart);
+  jb.L = jb.prefix + (uint64_t)((int64_t)(jb.end - sd->seg_base) - dstart);
   jb.nblocks = jb.fin ? (uint32_t)((jb.L + 8) / 64 + 1) : (uint32_t)(jb.L / 64);
   return true;
 }

@@ -81,8 +81,17 @@ int bsg_close(bsg_ctx* ctx);
 /* Number of finished chunks not yet drained, and drain up to cap of them (stream order). */
 size_t bsg_pending(const bsg_ctx* ctx);
 size_t bsg_drain(bsg_ctx* ctx, bsg_chunk* out, size_t cap);
-/* Staging tile size in bytes (default 256 MiB); call before the first write. */
+/* Staging tile size in bytes (default 256 MiB); call before the first write. Three tiles are
+ * in flight at once (BSG_STREAM_SLOTS overrides): tile i+1's split starts as soon as tile i's
+ * boundaries are known, while tile i's SHA-256 is still running. */
 int bsg_set_tile(bsg_ctx* ctx, size_t tile_bytes);
+/* Longest open chunk carried between tiles as bytes on the device (default 8 MiB); a longer
+ * one is carried as a SHA-256 midstate, which makes the next tile wait for this tile's hashes.
+ * 0 = always midstate (tests). Call before the first write. */
+int bsg_set_carry_cap(bsg_ctx* ctx, size_t bytes);
+/* Start a new stream on the same context (its device and pinned buffers are kept), as a
+ * pool of split.Writers would; undrained chunks of the previous stream are discarded. */
+int bsg_reset(bsg_ctx* ctx);
 void bsg_free(bsg_ctx* ctx);
 
 /* ---- device-resident batch of independent streams ---- */

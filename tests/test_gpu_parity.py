@@ -127,14 +127,18 @@ def test_dense_candidates_zero_runs(gpu, oracle, table):
 # --------------------------------------------------------------------------------------------
 # Streaming split.Writer path: arbitrary Write sizes, tiles carried across segments
 # --------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("tile", [4096, 5000, 65536 + 3, 1 << 20])
-def test_streaming_writer_vs_oracle(gpu, oracle, table, tile):
+@pytest.mark.parametrize("tile,carry_cap", [(4096, None), (5000, None), (65536 + 3, None),
+                                            (1 << 20, None), (4096, 0), (65536 + 3, 0),
+                                            (5000, 3000), (1 << 20, 40_000)])
+def test_streaming_writer_vs_oracle(gpu, oracle, table, tile, carry_cap):
+    """carry_cap None: open chunks carried as device bytes (default 8 MiB cap); 0: always as a
+    SHA-256 midstate; small caps mix both (the mode changes from tile to tile)."""
     from bs_amd.synth import splitmix_bytes
     data = splitmix_bytes(4242, 3_000_017)
     data = data[:1_500_000] + bytes(70_000) + data[1_500_000:]  # a dense stretch
     rng = np.random.default_rng(tile)
     for bits, mn in ((16, 1024), (10, 64)):
-        w = gpu.StreamingSplitter(bits=bits, min_size=mn, tile=tile)
+        w = gpu.StreamingSplitter(bits=bits, min_size=mn, tile=tile, carry_cap=carry_cap)
         pos, got = 0, []
         while pos < len(data):
             k = int(rng.choice([1, 7, 100, 4096, 32768, 300_000]))
@@ -146,6 +150,23 @@ def test_streaming_writer_vs_oracle(gpu, oracle, table, tile):
         w.free()
         ch = np.concatenate(got)
         assert as_tuples(ch) == as_tuples(oracle.split(table, data, bits=bits, min_size=mn))
+
+
+@pytest.mark.parametrize("carry_cap", [None, 0])
+def test_streaming_tile_multiples(gpu, oracle, table, carry_cap):
+    """Streams that end exactly on a tile boundary (the final segment is empty) and chunks far
+    longer than a tile (bits=20: mean chunk 1 MiB over 64 KiB tiles)."""
+    from bs_amd.synth import splitmix_bytes
+    tile = 65536
+    for n, bits in ((4 * tile, 16), (tile, 16), (40 * tile, 20), (40 * tile + 1, 20)):
+        d = splitmix_bytes(n + bits, n)
+        w = gpu.StreamingSplitter(bits=bits, min_size=1024, tile=tile, carry_cap=carry_cap)
+        w.write(d[: n // 3])
+        w.write(d[n // 3:])
+        w.close()
+        ch = w.drain()
+        w.free()
+        assert as_tuples(ch) == as_tuples(oracle.split(table, d, bits=bits, min_size=1024)), n
 
 
 def test_streaming_small_and_empty(gpu, oracle, table):
