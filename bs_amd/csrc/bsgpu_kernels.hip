@@ -1011,9 +1011,8 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     const uint32_t steps = min(B, nmax - base);
 #if BSG_BANK_ROUNDS
     const uint32_t* ones = ring + 64 * kLongRow;
-    for (uint32_t i = 0; i < steps; ++i)
-      sha256_rounds_skew(hs, bl.a_side ? ones : ring + (cR * B + i) * kLongRow, bl,
-                         base + i < nb);
+    sha256_blocks_skew(hs, bl.a_side ? ones : ring + cR * B * kLongRow,
+                       bl.a_side ? 0u : 4u * kLongRow, steps, (int32_t)nb - (int32_t)base, bl);
 #else
     for (uint32_t i = 0; i < steps; ++i) {
       const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + (cR * B + i) * kLongRow);

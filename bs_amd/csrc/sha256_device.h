@@ -306,4 +306,27 @@ __device__ __forceinline__ void sha256_rounds_skew(uint32_t (&hs)[4], const uint
   }
 }
 
+// `nblk` consecutive blocks (wave-uniform) of the skewed pairs, block k's K+W row at
+// row + k * stride bytes (A lanes: stride 0 on their row of ones), as one asm loop
+// (tools/gen_skew_asm.py, main_loop). A lane pair whose chain has only `lim` blocks left stops
+// after them (exec-masked), keeping its final state in hs.
+#include "sha256_skew_loop.inc"
+__device__ __forceinline__ void sha256_blocks_skew(uint32_t (&hs)[4], const uint32_t* row,
+                                                   uint32_t stride, uint32_t nblk, int32_t lim,
+                                                   const SkewLane& b) {
+  if (nblk == 0) return;
+  const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const uint32_t*)row);
+  const uint64_t amask = 0xAAAAAAAAAAAAAAAAull;  // A lanes: odd
+  uint32_t cnt;
+  uint64_t sexec;
+  asm volatile(BSG_SKEW_LOOP_ASM
+               : [h0] "+v"(hs[0]), [h1] "+v"(hs[1]), [h2] "+v"(hs[2]), [h3] "+v"(hs[3]),
+                 [cnt] "=&s"(cnt), [sexec] "=&s"(sexec)
+               : [addr] "v"(addr), [stride] "v"(stride), [nblk] "s"(nblk), [lim] "v"(lim),
+                 [xm] "v"(b.xm), [s1] "v"(b.rot1), [s2] "v"(b.rot2), [s3] "v"(b.rot3),
+                 [amask] "s"(amask)
+               : "memory", BSG_SKEW_LOOP_CLOBBERS);
+}
+
 }  // namespace bsg

@@ -45,6 +45,16 @@ __global__ __launch_bounds__(64) void kb(uint64_t* out, uint32_t* io, int blocks
     STAMP(t1);
     if (threadIdx.x == 3 || threadIdx.x == 4)
       for (int k = 0; k < 4; ++k) io[2000 + (threadIdx.x == 4 ? k : 4 + k)] = hs[k];
+  } else if (V == 3) {  // skewed pair, whole block loop in one asm statement
+    const SkewLane sl = skew_lane();
+    uint32_t hs[4];
+    const int emap[4] = {6, 7, 4, 5};
+    for (int k = 0; k < 4; ++k) hs[k] = sl.a_side ? st[k] : st[emap[k]];
+    STAMP(t0);
+    sha256_blocks_skew(hs, rows[sl.a_side ? 1 : 0], 0u, (uint32_t)blocks, blocks, sl);
+    STAMP(t1);
+    if (threadIdx.x == 0 || threadIdx.x == 1)
+      for (int k = 0; k < 4; ++k) io[2000 + (threadIdx.x == 1 ? k : emap[k])] = hs[k];
   } else if (V >= 10) {  // instruction-order variants of the skewed pair (tools/gen_skew_asm.py)
     const SkewLane sl = skew_lane();
     uint32_t hs[4];
@@ -120,6 +130,7 @@ int main() {
   run<0>("single lane (14 VALU/round)", ref);
   run<1>("banked pair (10 VALU + s_nop)", ref);
   run<2>("skewed pair (9 VALU/round)", ref);
+  run<3>("skewed pair, asm block loop", ref);
   run<10>("skew order A: xad al0 al1 dpp al2 bx xor3 ch", ref);
   run<11>("skew order B: xad dpp al0 al1 al2 bx xor3 ch", ref);
   run<12>("skew order C: al0 al1 al2 bx xad dpp xor3 ch", ref);
