@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--min-size", type=int, default=1024)
     ap.add_argument("--cpu-sample-mib", type=int, default=1024,
                     help="bytes of stream 0 the CPU oracle baseline splits+hashes (0: skip)")
+    ap.add_argument("--e2e-mib", type=int, default=1024,
+                    help="bytes of host-memory stream for the PCIe-inclusive streaming rate "
+                         "(bsg_write -> records in host memory; 0: skip)")
     ap.add_argument("--check", action="store_true",
                     help="verify the device records against the CPU oracle after timing")
     return ap.parse_args()
@@ -108,6 +111,54 @@ def cpu_baseline(sample_mib: int, bits: int, min_size: int) -> dict | None:
     return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"first {sample_mib} MiB of stream 0 (same bytes/params), C oracle "
                       f"split+sha256, 1 thread, {len(ch)} chunks in {dt:.2f}s"}
+
+
+def chain_roofline(diag: dict) -> dict | None:
+    """k_sha's real bound: the longest chunk's serial SHA-256 chain. Floor = 66 iterations x 9
+    VALU per 64-round block (sha256_skew_loop.inc) at the SIMD's 4 cycles per wave64 VALU
+    instruction; achieved = the in-kernel s_memtime cycles per block of the longest job."""
+    try:
+        cyc = float(diag["long"]["cycles_per_block"])
+    except (KeyError, TypeError, ValueError):
+        return None
+    if cyc <= 0:
+        return None
+    floor = 66 * 9 * 4.0
+    return {"bound": "issue (serial chain)", "kernel": "k_sha wave mode",
+            "floor_cycles_per_block": floor, "achieved_cycles_per_block": round(cyc, 1),
+            "frac": round(floor / cyc, 4), "blocks": diag["long"].get("blocks")}
+
+
+def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
+    """The streaming path from host memory: bsg_write of 32 MiB pieces (copy into pinned
+    staging, hipMemcpyAsync H2D per 256 MiB tile, three tiles in flight) -> split + SHA-256 ->
+    records D2H -> bsg_drain. Best of 2 after one warm-up on the same context (bsg_reset)."""
+    if mib <= 0:
+        return None
+    from bs_amd import bsgpu
+    from bs_amd.synth import splitmix_array
+    n = mib << 20
+    data = splitmix_array(BASE_SEED, n)
+    mv = memoryview(data)
+    piece = 32 << 20
+    w = bsgpu.StreamingSplitter(bits=bits, min_size=min_size, device=device)
+    best, nch = None, 0
+    for rep in range(3):
+        w.reset()
+        t0 = time.perf_counter()
+        nch = 0
+        for i in range(0, n, piece):
+            w.write(mv[i:i + piece])
+            nch += len(w.drain())
+        w.close()
+        nch += len(w.drain())
+        dt = time.perf_counter() - t0
+        if rep and (best is None or dt < best):
+            best = dt
+    w.free()
+    return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "chunks": nch,
+            "path": "host memory -> bsg_write (pinned staging, H2D) -> split + SHA-256 -> "
+                    "records in host memory; tile 256 MiB, 3 tiles in flight"}
 
 
 KERNEL_NAMES = {"k_scan": "bsg::k_scan(bsg::ScanArgs)", "k_sha": "bsg::k_sha(bsg::ShaArgs)"}
@@ -190,11 +241,14 @@ def main():
                      and (got["offset"] == ref["offset"]).all())
     cpu = cpu_baseline(args.cpu_sample_mib, args.bits, args.min_size) \
         if (rank == 0 and world == 1) else None
+    e2e = end_to_end(args.e2e_mib, args.bits, args.min_size, local) \
+        if (rank == 0 and world == 1) else None
     workload = ("configs[1]: 1 GiB random stream per GPU, default split params"
                 if (ns == 1 and nbytes == 1 << 30 and args.bits == 16 and args.min_size == 1024)
                 else f"{ns} x {args.stream_mib} MiB streams per GPU")
     traffic, traffic_src = pmc_traffic(names[dom], workload)
     scan_gbs = per_launch_bytes / (stage_avg[0] * 1e-3) / 1e9 if stage_avg[0] > 0 else 0.0
+    diag = eng.diag()
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -222,9 +276,11 @@ def main():
                          "k_scan": {"achieved": round(scan_gbs, 1),
                                     "frac": round(scan_gbs / HBM_PEAK_GBS, 4)}},
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
             "stage_ms": {n: round(v, 4) for n, v in zip(names, stage_avg)},
             "chunks_per_step": int(chunks),
-            "sha_path": eng.diag(),
+            "sha_path": diag,
+            "chain_roofline": chain_roofline(diag),
         }
         if check is not None:
             line["oracle_check"] = check
