@@ -11,6 +11,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "../../include/bs_split.hpp"
 
@@ -28,12 +31,23 @@ std::string RefString(const Ref& r) {
   return s;
 }
 
-Status GpuHasher::Sum(const uint8_t* data, size_t n, Ref* out) {
+GpuHasher::~GpuHasher() { bsg_hasher_free(h_); }
+
+Status GpuHasher::SumBatch(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                           size_t n, Ref* refs) {
+  if (n == 0) return Status::Ok();
   std::lock_guard<std::mutex> g(mu_);
-  const uint64_t off = 0, len = n;
+  if (!h_ && !(h_ = bsg_hasher_new(device_))) return Status::Err(BSG_EDEVICE, "bsg_hasher_new");
   static const uint8_t empty = 0;
-  int rc = bsg_sha256_batch(device_, n ? data : &empty, &off, &len, 1, out->data());
+  static_assert(sizeof(Ref) == 32, "Ref is 32 packed bytes");
+  int rc = bsg_hasher_sum(h_, base ? base : &empty, off, len, (uint32_t)n,
+                          reinterpret_cast<uint8_t*>(refs));
   return rc ? Status::Err(rc, std::string("sha256: ") + bsg_errstr(rc)) : Status::Ok();
+}
+
+Status GpuHasher::Sum(const uint8_t* data, size_t n, Ref* out) {
+  const uint64_t off = 0, len = n;
+  return SumBatch(data, &off, &len, 1, out);
 }
 
 Status MemStore::Get(const Ref& ref, std::vector<uint8_t>* out) {
@@ -197,6 +211,60 @@ struct Writer::TBNode {   // hashsplit.TreeBuilderNode
   uint64_t size = 0, offset = 0;
 };
 
+Writer::Writer(int device) : hasher_(device) {}
+
+// A process-wide pool of streaming contexts, keyed by (device, bits, min_size, tile): a
+// split.Writer per file (fs.Dir.AddDir) would otherwise pay for three engines and their pinned
+// staging on every NewWriter. A context goes back with bsg_reset when its Writer is destroyed.
+namespace {
+struct CtxKey {
+  int device;
+  uint32_t bits, min_size;
+  size_t tile;
+  bool operator<(const CtxKey& o) const {
+    return std::tie(device, bits, min_size, tile) < std::tie(o.device, o.bits, o.min_size, o.tile);
+  }
+};
+std::mutex g_pool_mu;
+std::map<CtxKey, std::vector<bsg_ctx*>>& ctx_pool() {
+  static auto* pool = new std::map<CtxKey, std::vector<bsg_ctx*>>();  // never destroyed:
+  return *pool;  // pooled contexts live until exit (their HIP runtime may be torn down first)
+}
+constexpr size_t kPoolPerKey = 4;
+
+bsg_ctx* ctx_acquire(const CtxKey& k, const bsg_params* p, int* rc) {
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    auto& v = ctx_pool()[k];
+    if (!v.empty()) {
+      bsg_ctx* c = v.back();
+      v.pop_back();
+      *rc = BSG_OK;
+      return c;
+    }
+  }
+  bsg_ctx* c = bsg_open(k.device, p, nullptr, rc);
+  if (c && k.tile && (*rc = bsg_set_tile(c, k.tile)) != BSG_OK) {
+    bsg_free(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void ctx_release(const CtxKey& k, bsg_ctx* c) {
+  if (!c) return;
+  if (bsg_reset(c) == BSG_OK) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    auto& v = ctx_pool()[k];
+    if (v.size() < kPoolPerKey) {
+      v.push_back(c);
+      return;
+    }
+  }
+  bsg_free(c);
+}
+}  // namespace
+
 std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) {
   Status dummy;
   if (!err) err = &dummy;
@@ -204,7 +272,7 @@ std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) 
     *err = Status::Err(BSG_EINVAL, "nil store");
     return nullptr;
   }
-  std::unique_ptr<Writer> w(new Writer());
+  std::unique_ptr<Writer> w(new Writer(opt.device));
   w->st_ = st;
   w->rp_ = dynamic_cast<RefPutter*>(st);
   w->opt_ = opt;
@@ -215,13 +283,9 @@ std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) 
   p.fanout = w->opt_.fanout;
   p.reserved = 0;
   int rc = 0;
-  w->ctx_ = bsg_open(opt.device, &p, nullptr, &rc);
+  w->ctx_ = ctx_acquire(CtxKey{opt.device, p.split_bits, p.min_size, opt.tile}, &p, &rc);
   if (!w->ctx_) {
     *err = Status::Err(rc, std::string("bsg_open: ") + bsg_errstr(rc));
-    return nullptr;
-  }
-  if (opt.tile && (rc = bsg_set_tile(w->ctx_, opt.tile))) {
-    *err = Status::Err(rc, "bsg_set_tile");
     return nullptr;
   }
   *err = Status::Ok();
@@ -229,13 +293,49 @@ std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) 
 }
 
 Writer::~Writer() {
-  if (ctx_) bsg_free(ctx_);
+  if (ctx_)
+    ctx_release(CtxKey{opt_.device, opt_.bits, (uint32_t)std::max(opt_.min_size, 0), opt_.tile},
+                ctx_);
 }
 
 Status Writer::PutProto(const Node& node, Ref* ref) {
   const std::string b = node.Marshal();
   bool added;
+  if (rp_) {
+    Status s = hasher_.Sum(reinterpret_cast<const uint8_t*>(b.data()), b.size(), ref);
+    if (!s.ok()) return s;
+    return rp_->PutWithRef(*ref, reinterpret_cast<const uint8_t*>(b.data()), b.size(), &added);
+  }
   return st_->Put(reinterpret_cast<const uint8_t*>(b.data()), b.size(), ref, &added);
+}
+
+Status Writer::PutProtos(const std::vector<const Node*>& nodes, std::vector<Ref>* refs) {
+  refs->assign(nodes.size(), Ref{});
+  if (!rp_) {  // the store hashes each blob itself
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      Status s = PutProto(*nodes[i], &(*refs)[i]);
+      if (!s.ok()) return s;
+    }
+    return Status::Ok();
+  }
+  std::string packed;
+  std::vector<uint64_t> off(nodes.size()), len(nodes.size());
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const std::string b = nodes[i]->Marshal();
+    off[i] = packed.size();
+    len[i] = b.size();
+    packed += b;
+  }
+  Status s = hasher_.SumBatch(reinterpret_cast<const uint8_t*>(packed.data()), off.data(),
+                              len.data(), nodes.size(), refs->data());
+  if (!s.ok()) return s;
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    bool added;
+    s = rp_->PutWithRef((*refs)[i], reinterpret_cast<const uint8_t*>(packed.data()) + off[i],
+                        len[i], &added);
+    if (!s.ok()) return s;
+  }
+  return Status::Ok();
 }
 
 Status Writer::F(TBNode& n, std::shared_ptr<Wrapped>* out) {  // split/split.go:52-81
@@ -243,12 +343,14 @@ Status Writer::F(TBNode& n, std::shared_ptr<Wrapped>* out) {  // split/split.go:
   uint64_t offset = n.offset;
   w->node.offset = n.offset;
   w->node.size = n.size;
-  for (const auto& child : n.nodes) {
-    Ref ref;
-    Status s = PutProto(child->node, &ref);
-    if (!s.ok()) return s;
-    w->node.nodes.push_back(Child{ref, offset});
-    offset += child->node.size;
+  std::vector<const Node*> kids;
+  for (const auto& child : n.nodes) kids.push_back(&child->node);
+  std::vector<Ref> refs;
+  Status s = PutProtos(kids, &refs);  // split.go:61-69, all children in one GPU call
+  if (!s.ok()) return s;
+  for (size_t i = 0; i < n.nodes.size(); ++i) {
+    w->node.nodes.push_back(Child{refs[i], offset});
+    offset += n.nodes[i]->node.size;
   }
   for (const Child& c : n.chunks) {  // chunks were Put on arrival; c.offset holds the length
     w->node.leaves.push_back(Child{c.ref, offset});
@@ -287,23 +389,38 @@ Status Writer::Drain() {
   const size_t got = bsg_drain(ctx_, drained_.data(), n);
   for (size_t i = 0; i < got; ++i) {
     const bsg_chunk& c = drained_[i];
-    if (c.offset != base_ + head_ || c.offset + c.len > base_ + buf_.size())
+    if (c.offset != emitted_ || c.offset + c.len > end_)
       return Status::Err(BSG_EDEVICE, "chunk records out of order");
-    const uint8_t* bytes = buf_.data() + head_;
+    // the chunk's bytes: in place if one piece holds them, else gathered into span_
+    const uint8_t* bytes = nullptr;
+    uint64_t skip = c.offset - base_;
+    size_t k = 0;
+    while (skip >= pieces_[k].size()) skip -= pieces_[k++].size();
+    if (skip + c.len <= pieces_[k].size()) {
+      bytes = pieces_[k].data() + skip;
+    } else {
+      span_.resize(c.len);
+      uint64_t done = 0;
+      for (; done < c.len; ++k, skip = 0) {
+        const uint64_t take = std::min<uint64_t>(c.len - done, pieces_[k].size() - skip);
+        std::memcpy(span_.data() + done, pieces_[k].data() + skip, take);
+        done += take;
+      }
+      bytes = span_.data();
+    }
     Ref ref;
     std::memcpy(ref.data(), c.ref, 32);
     bool added;
     Status s = rp_ ? rp_->PutWithRef(ref, bytes, c.len, &added)  // GPU ref, no re-hash
                    : st_->Put(bytes, c.len, &ref, &added);       // store computes the ref
     if (!s.ok()) return s;
-    head_ += c.len;
+    emitted_ += c.len;
+    while (!pieces_.empty() && base_ + pieces_.front().size() <= emitted_) {  // fully emitted
+      base_ += pieces_.front().size();
+      pieces_.pop_front();
+    }
     s = Add(ref, c.len, c.level / opt_.fanout);  // split/split.go:86
     if (!s.ok()) return s;
-  }
-  if (head_ > (1u << 20) && head_ * 2 > buf_.size()) {  // compact the emitted prefix
-    buf_.erase(buf_.begin(), buf_.begin() + head_);
-    base_ += head_;
-    head_ = 0;
   }
   return Status::Ok();
 }
@@ -312,7 +429,10 @@ Status Writer::Write(const uint8_t* p, size_t n, size_t* written) {
   if (written) *written = 0;
   if (closed_) return Status::Err(BSG_ESTATE, "write after close");
   if (!sticky_.ok()) return sticky_;
-  buf_.insert(buf_.end(), p, p + n);
+  if (n) {
+    pieces_.emplace_back(p, p + n);
+    end_ += n;
+  }
   int rc = bsg_write(ctx_, p, n);
   if (rc) return sticky_ = Status::Err(rc, std::string("bsg_write: ") + bsg_errstr(rc));
   Status s = Drain();

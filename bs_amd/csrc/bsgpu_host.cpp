@@ -1059,47 +1059,98 @@ int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed
   return BSG_OK;
 }
 
+}  // extern "C"
+
+// Batched Blob.Ref() with persistent device buffers and stream (bsg_hasher_*): a Writer hashes
+// every tree node through one, so a call costs one H2D, one launch and one D2H, not four
+// allocations.
+struct bsg_hasher {
+  int dev = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  DevBuf data, off, len, refs;
+  PinBuf h_meta;  // off[n] | len[n] staged for one H2D
+
+  int sum(const uint8_t* base, const uint64_t* o, const uint64_t* l, uint32_t n, uint8_t* out) {
+    hipPointerAttribute_t attr;
+    bool on_device = false;
+    if (hipPointerGetAttributes(&attr, base) == hipSuccess)
+      on_device = (attr.type == hipMemoryTypeDevice);
+    else
+      (void)hipGetLastError();
+    uint64_t hi = 0;
+    for (uint32_t i = 0; i < n; ++i) hi = std::max<uint64_t>(hi, o[i] + l[i]);
+    // always hash from a private copy with kReadSlack bytes of tail padding
+    HCHECK(data.ensure(hi + kReadSlack));
+    HCHECK(off.ensure(8ull * n));
+    HCHECK(len.ensure(8ull * n));
+    HCHECK(refs.ensure(32ull * n));
+    HCHECK(h_meta.ensure(16ull * n));
+    std::memcpy(h_meta.p, o, 8ull * n);
+    std::memcpy(h_meta.as<uint8_t>() + 8ull * n, l, 8ull * n);
+    if (hi)
+      HCHECK(hipMemcpyAsync(data.p, base, hi,
+                            on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, stream));
+    HCHECK(hipMemcpyAsync(off.p, h_meta.p, 8ull * n, hipMemcpyHostToDevice, stream));
+    HCHECK(hipMemcpyAsync(len.p, h_meta.as<uint8_t>() + 8ull * n, 8ull * n,
+                          hipMemcpyHostToDevice, stream));
+    BlobShaArgs a{data.as<uint8_t>(), off.as<uint64_t>(), len.as<uint64_t>(), n,
+                  refs.as<uint8_t>()};
+    HCHECK(launch_sha_blobs(a, stream, num_cus));
+    HCHECK(hipMemcpyAsync(out, refs.p, 32ull * n, hipMemcpyDeviceToHost, stream));
+    HCHECK(hipStreamSynchronize(stream));
+    return BSG_OK;
+  }
+};
+
+extern "C" {
+
+bsg_hasher* bsg_hasher_new(int device) {
+  if (device < 0 || device >= bsg_device_count() || hipSetDevice(device) != hipSuccess)
+    return nullptr;
+  bsg_hasher* h = new (std::nothrow) bsg_hasher();
+  if (!h) return nullptr;
+  h->dev = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    h->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+int bsg_hasher_sum(bsg_hasher* h, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                   uint32_t n, uint8_t* refs) {
+  if (!h || (n && (!base || !off || !len || !refs))) return BSG_EINVAL;
+  if (n == 0) return BSG_OK;
+  HCHECK(hipSetDevice(h->dev));
+  return h->sum(base, off, len, n, refs);
+}
+
+void bsg_hasher_free(bsg_hasher* h) {
+  if (!h) return;
+  hipSetDevice(h->dev);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  h->data.release();
+  h->off.release();
+  h->len.release();
+  h->refs.release();
+  h->h_meta.release();
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
 int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                      uint32_t n, uint8_t* refs) {
   if (n && (!base || !off || !len || !refs)) return BSG_EINVAL;
   if (n == 0) return BSG_OK;
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
-  HCHECK(hipSetDevice(device));
-  hipPointerAttribute_t attr;
-  bool on_device = false;
-  if (hipPointerGetAttributes(&attr, base) == hipSuccess)
-    on_device = (attr.type == hipMemoryTypeDevice);
-  else
-    (void)hipGetLastError();
-  uint64_t hi = 0;
-  for (uint32_t i = 0; i < n; ++i) hi = std::max<uint64_t>(hi, off[i] + len[i]);
-  // always hash from a private copy with kReadSlack bytes of tail padding
-  DevBuf dd, doff, dlen, drefs;
-  int rc = BSG_OK;
-  if (dd.ensure(hi + kReadSlack) != hipSuccess) return BSG_ENOMEM;
-  if (hi && hipMemcpy(dd.p, base, hi, on_device ? hipMemcpyDeviceToDevice
-                                                : hipMemcpyHostToDevice) != hipSuccess)
-    rc = BSG_EDEVICE;
-  const uint8_t* dbase = dd.as<uint8_t>();
-  if (rc == BSG_OK && (doff.ensure(8ull * n) != hipSuccess || dlen.ensure(8ull * n) != hipSuccess ||
-                       drefs.ensure(32ull * n) != hipSuccess))
-    rc = BSG_ENOMEM;
-  if (rc == BSG_OK && (hipMemcpy(doff.p, off, 8ull * n, hipMemcpyHostToDevice) != hipSuccess ||
-                       hipMemcpy(dlen.p, len, 8ull * n, hipMemcpyHostToDevice) != hipSuccess))
-    rc = BSG_EDEVICE;
-  if (rc == BSG_OK) {
-    hipDeviceProp_t prop;
-    int cus = 256;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
-    BlobShaArgs a{dbase, doff.as<uint64_t>(), dlen.as<uint64_t>(), n, drefs.as<uint8_t>()};
-    if (launch_sha_blobs(a, nullptr, cus) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(refs, drefs.p, 32ull * n, hipMemcpyDeviceToHost) != hipSuccess)
-      rc = BSG_EDEVICE;
-  }
-  dd.release();
-  doff.release();
-  dlen.release();
-  drefs.release();
+  bsg_hasher* h = bsg_hasher_new(device);
+  if (!h) return BSG_EDEVICE;
+  const int rc = h->sum(base, off, len, n, refs);
+  bsg_hasher_free(h);
   return rc;
 }
 

@@ -15,6 +15,7 @@
 #pragma once
 
 #include <array>
+#include <deque>
 #include <cstddef>
 #include <cstdint>
 #include <functional>
@@ -61,15 +62,23 @@ class RefPutter {
   virtual Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) = 0;
 };
 
-// Batched/one-off SHA-256 of host bytes on the GPU (persistent device buffers + stream).
+// Batched/one-off SHA-256 of host bytes on the GPU (bsg_hasher: persistent device buffers +
+// stream, created on first use).
 class GpuHasher {
  public:
   explicit GpuHasher(int device = 0) : device_(device) {}
+  ~GpuHasher();
+  GpuHasher(const GpuHasher&) = delete;
+  GpuHasher& operator=(const GpuHasher&) = delete;
   Status Sum(const uint8_t* data, size_t n, Ref* out);
+  // refs[i] = SHA-256 of base[off[i] .. off[i] + len[i]) for n blobs, one GPU call.
+  Status SumBatch(const uint8_t* base, const uint64_t* off, const uint64_t* len, size_t n,
+                  Ref* refs);
 
  private:
   int device_;
   std::mutex mu_;
+  bsg_hasher* h_ = nullptr;
 };
 
 class MemStore : public Store, public RefPutter {
@@ -148,19 +157,26 @@ class Writer {
   struct Wrapped;
 
  private:
-  Writer() = default;
+  explicit Writer(int device);
   Status Drain();
   Status Add(const Ref& ref, uint64_t len, unsigned level);  // hashsplit TreeBuilder.Add
   Status F(TBNode& n, std::shared_ptr<Wrapped>* out);        // split.go:52-81
   Status PutProto(const Node& node, Ref* ref);               // proto.go:22-29
+  // PutProto of several nodes: one batched GPU hash when the store takes refs (RefPutter).
+  Status PutProtos(const std::vector<const Node*>& nodes, std::vector<Ref>* refs);
+  GpuHasher hasher_;
 
   Store* st_ = nullptr;
   RefPutter* rp_ = nullptr;
   Options opt_;
   bsg_ctx* ctx_ = nullptr;
-  std::vector<uint8_t> buf_;  // stream bytes not yet emitted as chunks
-  size_t head_ = 0;           // emitted prefix of buf_
-  uint64_t base_ = 0;         // stream offset of buf_[0]
+  // Stream bytes not yet emitted as chunks, kept as the Write() pieces they arrived in: a
+  // piece is dropped once every byte of it is in an emitted chunk, so nothing is ever moved.
+  std::deque<std::vector<uint8_t>> pieces_;
+  uint64_t base_ = 0;          // stream offset of pieces_.front()[0]
+  uint64_t end_ = 0;           // stream offset one past the last byte written
+  uint64_t emitted_ = 0;       // stream offset of the next chunk to emit
+  std::vector<uint8_t> span_;  // scratch for a chunk that spans pieces
   std::vector<std::unique_ptr<TBNode>> levels_;
   std::vector<bsg_chunk> drained_;
   Ref root_{};

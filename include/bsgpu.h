@@ -140,6 +140,14 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
 int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                      uint32_t n, uint8_t* refs);
 
+/* The same with persistent device buffers and a HIP stream of its own (one per thread at a
+ * time), for callers that hash many small batches (tree nodes, store Puts). */
+typedef struct bsg_hasher bsg_hasher;
+bsg_hasher* bsg_hasher_new(int device);
+int bsg_hasher_sum(bsg_hasher* h, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                   uint32_t n, uint8_t* refs);
+void bsg_hasher_free(bsg_hasher* h);
+
 /* Device memory helpers (so callers need no second HIP runtime): kind 0 = H2D, 1 = D2H,
  * 2 = D2D. */
 void* bsg_device_malloc(int device, size_t bytes);
