@@ -169,6 +169,20 @@ def test_streaming_tile_multiples(gpu, oracle, table, carry_cap):
         assert as_tuples(ch) == as_tuples(oracle.split(table, d, bits=bits, min_size=1024)), n
 
 
+def test_streaming_candidate_overflow(gpu, oracle, table):
+    """Every byte a candidate (zeros, bits=1): the first run of each tile overflows the
+    candidate buffer and is re-run at its exact size inside the pipeline."""
+    from bs_amd.synth import splitmix_bytes
+    d = bytes(600_000) + splitmix_bytes(5, 300_000) + bytes(500_000)
+    w = gpu.StreamingSplitter(bits=1, min_size=64, tile=1 << 19)
+    for i in range(0, len(d), 100_000):
+        w.write(d[i:i + 100_000])
+    w.close()
+    ch = w.drain()
+    w.free()
+    assert as_tuples(ch) == as_tuples(oracle.split(table, d, bits=1, min_size=64))
+
+
 def test_streaming_small_and_empty(gpu, oracle, table):
     for n in (0, 1, 63, 64, 1023, 1024, 1025, 4095, 4096, 4097):
         from bs_amd.synth import splitmix_bytes
