@@ -351,6 +351,16 @@ struct bsg_engine {
 // tile i+1 waits for tile i's k_sha and continues from the exported midstate.
 // Records complete in tile order; bsg_pending/bsg_drain hand them out in stream order.
 // ------------------------------------------------------------------------------------------
+// Host threads copying a large Write into pinned staging (BSG_COPY_THREADS, default 8).
+int copy_threads() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("BSG_COPY_THREADS");
+    v = e ? std::max(1, std::min(64, std::atoi(e))) : 8;
+  }
+  return v;
+}
+
 constexpr int kMaxSlots = 8;
 constexpr uint64_t kDefaultCarryCap = 8ull << 20;
 // Tiles in flight. Each has its own HIP stream, and streams beyond the process's hardware
@@ -624,7 +634,7 @@ struct bsg_ctx {
   static void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
     constexpr size_t kPiece = 2ull << 20;  // per thread, at least
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned nt = (unsigned)std::min<size_t>({(size_t)8, (size_t)hw, n / kPiece});
+    const unsigned nt = (unsigned)std::min<size_t>({(size_t)copy_threads(), (size_t)hw, n / kPiece});
     if (nt <= 1) {
       std::memcpy(dst, src, n);
       return;

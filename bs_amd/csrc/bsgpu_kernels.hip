@@ -1086,9 +1086,16 @@ __global__ __launch_bounds__(256, 1) void k_sha(ShaArgs a) {
   // break; }` form was restructured by hipcc into a nested loop that re-entered job 0 forever.
   const uint64_t ntickets = a.ctr->ntickets;
   uint64_t t = pop_uniform(&a.ctr->long_head);
-  while (t < ntickets) {
-    sha_wave_job(a, M, t, nlong, ring);
-    t = pop_uniform(&a.ctr->long_head);
+  if (t < ntickets) {
+    // A long chain is the launch's critical path. When another kernel's waves share its SIMD
+    // (the streaming pipeline runs the next tile's scan beside this k_sha), the arbiter should
+    // issue the chain's instructions first.
+    __builtin_amdgcn_s_setprio(3);
+    while (t < ntickets) {
+      sha_wave_job(a, M, t, nlong, ring);
+      t = pop_uniform(&a.ctr->long_head);
+    }
+    __builtin_amdgcn_s_setprio(0);
   }
   sha_lane_mode(a, M);
 }
