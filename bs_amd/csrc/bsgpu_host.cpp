@@ -61,6 +61,15 @@ struct DevBuf {
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
+  // the device-side address of p (kernels write results straight into pinned host memory)
+  void* dev() const {
+    void* d = nullptr;
+    if (p && hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      d = nullptr;
+    }
+    return d;
+  }
   hipError_t ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes <= cap) return hipSuccess;
@@ -278,13 +287,13 @@ struct bsg_engine {
                  bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
                  last_end.as<uint64_t>(), chunk_cap, p, dctr};
     HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, ns, stream, num_cus)));
-    if (snapshot) {
+    if (snapshot) {  // by kernel, not by the copy engine (see launch_copy_out)
       HCHECK(h_snap.ensure(sizeof(Counters) + 8ull * (ns ? ns : 1)));
       if (!sel_ev) HCHECK(hipEventCreateWithFlags(&sel_ev, hipEventDisableTiming));
-      HCHECK(hipMemcpyAsync(h_snap.p, ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, stream));
-      if (ns)
-        HCHECK(hipMemcpyAsync(static_cast<uint8_t*>(h_snap.p) + sizeof(Counters), last_end.p,
-                              8ull * ns, hipMemcpyDeviceToHost, stream));
+      uint8_t* hs = static_cast<uint8_t*>(h_snap.dev());
+      if (!hs) return BSG_EDEVICE;
+      HCHECK(launch_copy_out(ctr.p, hs, sizeof(Counters), stream));
+      if (ns) HCHECK(launch_copy_out(last_end.p, hs + sizeof(Counters), 8ull * ns, stream));
       HCHECK(hipEventRecord(sel_ev, stream));
     }
 
@@ -461,12 +470,15 @@ struct bsg_ctx {
     if (t.recs_enq) return BSG_OK;
     int rc = read_sel(i);
     if (rc) return rc;
+    // by kernel behind k_sha: a hipMemcpyAsync D2H queued here would wait for k_sha inside the
+    // shared copy-engine queue and hold up the next tiles' H2D copies behind it
     HCHECK(t.recs.ensure(sizeof(bsg_chunk) * (t.nchunks ? t.nchunks : 1)));
+    void* rd = t.recs.dev();
+    void* cd = t.eng->h_ctr.dev();
+    if (!rd || !cd) return BSG_EDEVICE;
     if (t.nchunks)
-      HCHECK(hipMemcpyAsync(t.recs.p, t.eng->out.p, sizeof(bsg_chunk) * t.nchunks,
-                            hipMemcpyDeviceToHost, t.eng->stream));
-    HCHECK(hipMemcpyAsync(t.eng->h_ctr.p, t.eng->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost,
-                          t.eng->stream));
+      HCHECK(launch_copy_out(t.eng->out.p, rd, sizeof(bsg_chunk) * t.nchunks, t.eng->stream));
+    HCHECK(launch_copy_out(t.eng->ctr.p, cd, sizeof(Counters), t.eng->stream));
     HCHECK(hipEventRecord(t.done_ev, t.eng->stream));
     t.recs_enq = true;
     return BSG_OK;
@@ -530,6 +542,8 @@ struct bsg_ctx {
     const int i = cur;
     TileSlot& t = slots[i];
     bsg_engine* e = t.eng;
+    int rc0 = reclaim(i);  // the engine and device slot of the tile kSlots back
+    if (rc0) return rc0;
     HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
     uint8_t* base = t.dbuf.as<uint8_t>();
     StreamDesc d{};
@@ -617,10 +631,10 @@ struct bsg_ctx {
       }
       TileSlot& t = slots[cur];
       if (fill == 0) {
-        int rc = reclaim(cur);
-        if (rc) return rc;
+        // the staging buffer is free once its last H2D has run; the slot's engine and device
+        // buffer are reclaimed only at submit(), so the host copy overlaps that tile's k_sha
         HCHECK(t.staging.ensure(tile));
-        HCHECK(hipEventSynchronize(t.h2d_ev));  // staging free once its H2D has run
+        HCHECK(hipEventSynchronize(t.h2d_ev));
       }
       const size_t k = std::min(n, tile - fill);
       par_copy(t.staging.as<uint8_t>() + fill, p, k);

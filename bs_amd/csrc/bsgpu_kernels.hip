@@ -1246,6 +1246,23 @@ hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, 
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void k_copy_out(const uint32_t* __restrict__ src,
+                                                  uint32_t* __restrict__ dst, uint64_t words) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
+    dst[i] = src[i];
+}
+
+hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
+  // every caller copies whole structs of 4-byte multiples (ChunkRec, Counters, u64 arrays)
+  const uint64_t words = bytes / 4;
+  if (words == 0) return hipSuccess;
+  const uint32_t grid = grid_for(words, 256, 64);
+  hipLaunchKernelGGL(k_copy_out, dim3(grid), dim3(256), 0, s,
+                     static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), words);
+  return hipGetLastError();
+}
+
 hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus) {
   const uint32_t grid = grid_for(a.n, 256, 8u * (uint32_t)num_cus);
   hipLaunchKernelGGL(k_sha_blobs, dim3(grid), dim3(256), 0, s, a);

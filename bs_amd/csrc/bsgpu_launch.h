@@ -104,6 +104,10 @@ hipError_t launch_init(const InitArgs& a, hipStream_t s);
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus);
+// Device -> pinned host bytes by a kernel on stream s (dst: the device alias of a hipHostMalloc
+// buffer). Unlike hipMemcpyAsync D2H, a kernel waiting in its own stream for the work before
+// it holds no place in the shared copy-engine queue, so it cannot stall other streams' H2D.
+hipError_t launch_copy_out(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 hipError_t launch_fill_splitmix(uint8_t* p, uint64_t n, uint64_t seed, hipStream_t s,
                                 int num_cus);
 
