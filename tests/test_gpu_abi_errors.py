@@ -1,0 +1,69 @@
+"""C-ABI error behaviour on the device (mirrors the reference's error conventions: Write after
+Close fails, a missing root fails NewReader with bs.ErrNotFound) and the persistent hasher."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_chunks(data: bytes, ch) -> None:
+    assert b"".join(data[int(c["offset"]):int(c["offset"] + c["len"])] for c in ch) == data
+    for c in ch:
+        blob = data[int(c["offset"]):int(c["offset"] + c["len"])]
+        assert bytes(c["ref"]) == hashlib.sha256(blob).digest()
+
+
+def test_write_after_close_and_late_knobs(gpu):
+    from bs_amd.synth import splitmix_bytes
+    L = gpu.lib()
+    a, b = splitmix_bytes(1, 300_000), splitmix_bytes(2, 200_000)
+    w = gpu.StreamingSplitter()
+    w.write(a)
+    assert L.bsg_set_tile(w.h, 1 << 20) == -22        # tile fixed once bytes arrived
+    assert L.bsg_set_carry_cap(w.h, 0) == -22
+    w.close()
+    assert L.bsg_write(w.h, b"y", 1) == -71           # BSG_ESTATE: Write after Close
+    assert L.bsg_close(w.h) == 0                      # Close is idempotent
+    _check_chunks(a, w.drain())
+    w.reset()                                         # a reset context takes a new stream
+    w.write(b)
+    w.close()
+    _check_chunks(b, w.drain())
+    w.free()
+
+
+def test_reader_missing_root(gpu):
+    st = gpu.MemStore()
+    with pytest.raises(gpu.BsgError) as ei:
+        gpu.Reader(st, bytes(32))
+    assert ei.value.code == gpu.NOT_FOUND
+
+
+def test_persistent_hasher_batches(gpu):
+    L = gpu.lib()
+    L.bsg_hasher_new.restype = ctypes.c_void_p
+    L.bsg_hasher_new.argtypes = [ctypes.c_int]
+    L.bsg_hasher_sum.restype = ctypes.c_int
+    L.bsg_hasher_sum.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    L.bsg_hasher_free.argtypes = [ctypes.c_void_p]
+    h = L.bsg_hasher_new(0)
+    assert h
+    rng = np.random.default_rng(11)
+    try:
+        for n in (1, 7, 300):  # the buffers grow and are reused across calls
+            blobs = [rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+                     for _ in range(n)]
+            packed = b"".join(blobs)
+            off = np.cumsum([0] + [len(b) for b in blobs[:-1]]).astype(np.uint64)
+            ln = np.array([len(b) for b in blobs], dtype=np.uint64)
+            out = ctypes.create_string_buffer(32 * n)
+            assert L.bsg_hasher_sum(h, packed or b"\0", off.ctypes.data, ln.ctypes.data, n,
+                                    out) == 0
+            assert [out.raw[32 * i:32 * i + 32] for i in range(n)] == \
+                [hashlib.sha256(b).digest() for b in blobs]
+    finally:
+        L.bsg_hasher_free(h)
