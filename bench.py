@@ -55,6 +55,10 @@ def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BSG_BENCH_SHARE_GPU") == "1":
+        # rehearsal of the N>1 path on a one-GPU box: every rank drives device 0 (never for
+        # reported numbers; the driver launches one rank per GPU)
+        local = 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
