@@ -73,6 +73,9 @@ def lib() -> ctypes.CDLL:
         "bsg_drain": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
         "bsg_set_tile": (ctypes.c_int, [vp, ctypes.c_size_t]),
         "bsg_set_carry_cap": (ctypes.c_int, [vp, ctypes.c_size_t]),
+        "bsg_write_window": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(ctypes.c_size_t)]),
+        "bsg_write_commit": (ctypes.c_int, [vp, ctypes.c_size_t]),
         "bsg_free": (None, [vp]),
         "bsg_reset": (ctypes.c_int, [vp]),
         "bsg_engine_create": (vp, [ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_int)]),
@@ -356,6 +359,50 @@ class StreamingSplitter:
 
     def reset(self) -> None:
         _check(lib().bsg_reset(self.h), "bsg_reset")
+
+    def window(self) -> memoryview:
+        """bsg_write_window: writable memoryview of pinned staging; fill, then commit(n)."""
+        p, cap = ctypes.c_void_p(), ctypes.c_size_t()
+        _check(lib().bsg_write_window(self.h, ctypes.byref(p), ctypes.byref(cap)),
+               "bsg_write_window")
+        return memoryview((ctypes.c_uint8 * cap.value).from_address(p.value)).cast("B")
+
+    def commit(self, n: int) -> None:
+        _check(lib().bsg_write_commit(self.h, n), "bsg_write_commit")
+
+    def pread_file(self, path: str, threads: int = 8, piece: int = 16 << 20) -> int:
+        """Reads a whole file straight into pinned staging with `threads` parallel preads per
+        staging window (the form a Go caller gets with io.ReaderAt and goroutines)."""
+        from concurrent.futures import ThreadPoolExecutor
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            size = os.fstat(fd).st_size
+            pos = 0
+            with ThreadPoolExecutor(threads) as ex:
+                while pos < size:
+                    win = self.window()
+                    n = min(len(win), size - pos)
+                    parts = [(o, min(piece, n - o)) for o in range(0, n, piece)]
+                    got = list(ex.map(lambda p: os.preadv(fd, [win[p[0]:p[0] + p[1]]], pos + p[0]),
+                                      parts))
+                    if sum(got) != n:
+                        raise OSError("short read")
+                    self.commit(n)
+                    pos += n
+            return pos
+        finally:
+            os.close(fd)
+
+    def read_from(self, f, piece: int = 32 << 20) -> int:
+        """Reads a file object to EOF straight into pinned staging (readinto); returns bytes."""
+        total = 0
+        while True:
+            win = self.window()
+            k = f.readinto(win[:piece])
+            if not k:
+                return total
+            self.commit(k)
+            total += k
 
     def drain(self) -> np.ndarray:
         n = lib().bsg_pending(self.h)

@@ -645,6 +645,42 @@ struct bsg_ctx {
     return poll();
   }
 
+  // Zero-copy form of write(): the caller fills pinned staging directly (an io.Reader reads
+  // into it), then commits. The window is the rest of the current tile.
+  int window(uint8_t** p, size_t* cap) {
+    if (fill == tile) {
+      // The caller may be at EOF, so this tile cannot be the last one submitted as non-final:
+      // hold its last bytes back for the next tile. (A final segment must hold at least one
+      // byte: the flush of the open chunk is emitted by the scan of the final segment's last
+      // strip, and an empty segment has none.)
+      constexpr size_t kHold = 4096;
+      uint8_t held[kHold];
+      const size_t hold = std::min(kHold, tile / 2);
+      std::memcpy(held, slots[cur].staging.as<uint8_t>() + tile - hold, hold);
+      fill = tile - hold;
+      int rc = submit(false);
+      if (rc) return rc;
+      TileSlot& n = slots[cur];
+      HCHECK(n.staging.ensure(tile));
+      HCHECK(hipEventSynchronize(n.h2d_ev));
+      std::memcpy(n.staging.p, held, hold);
+      fill = hold;
+    }
+    TileSlot& t = slots[cur];
+    if (fill == 0) {
+      HCHECK(t.staging.ensure(tile));
+      HCHECK(hipEventSynchronize(t.h2d_ev));
+    }
+    *p = t.staging.as<uint8_t>() + fill;
+    *cap = tile - fill;
+    return BSG_OK;
+  }
+  int commit(size_t n) {
+    if (n > tile - fill) return BSG_EINVAL;
+    fill += n;
+    return poll();
+  }
+
   static void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
     constexpr size_t kPiece = 2ull << 20;  // per thread, at least
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
@@ -951,6 +987,27 @@ int bsg_write(bsg_ctx* c, const uint8_t* p, size_t n) {
   if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
   c->started = true;
   int rc = c->write(p, n);
+  if (rc) c->sticky = rc;
+  return rc;
+}
+
+int bsg_write_window(bsg_ctx* c, uint8_t** p, size_t* cap) {
+  if (!c || !p || !cap) return BSG_EINVAL;
+  if (c->closed) return BSG_ESTATE;
+  if (c->sticky) return c->sticky;
+  if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
+  c->started = true;
+  int rc = c->window(p, cap);
+  if (rc) c->sticky = rc;
+  return rc;
+}
+
+int bsg_write_commit(bsg_ctx* c, size_t n) {
+  if (!c) return BSG_EINVAL;
+  if (c->closed) return BSG_ESTATE;
+  if (c->sticky) return c->sticky;
+  if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
+  int rc = c->commit(n);
   if (rc) c->sticky = rc;
   return rc;
 }

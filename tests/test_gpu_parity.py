@@ -183,6 +183,29 @@ def test_streaming_candidate_overflow(gpu, oracle, table):
     assert as_tuples(ch) == as_tuples(oracle.split(table, d, bits=1, min_size=64))
 
 
+def test_streaming_zero_copy_window(gpu, oracle, table, tmp_path):
+    """bsg_write_window/commit: a file read straight into pinned staging (io.Reader form)."""
+    from bs_amd.synth import splitmix_bytes
+    d = splitmix_bytes(77, 1_500_000)
+    f = tmp_path / "stream.bin"
+    f.write_bytes(d)
+    want = as_tuples(oracle.split(table, d, bits=12, min_size=256))
+    w = gpu.StreamingSplitter(bits=12, min_size=256, tile=1 << 18)
+    with open(f, "rb") as fh:
+        assert w.read_from(fh, piece=100_000) == len(d)
+    w.close()
+    assert as_tuples(w.drain()) == want
+    # a stream whose length is an exact multiple of the tile, read to EOF through the window
+    e = d[: 5 * (1 << 18)]
+    f.write_bytes(e)
+    w.reset()
+    with open(f, "rb") as fh:
+        assert w.read_from(fh, piece=1 << 18) == len(e)
+    w.close()
+    assert as_tuples(w.drain()) == as_tuples(oracle.split(table, e, bits=12, min_size=256))
+    w.free()
+
+
 def test_streaming_small_and_empty(gpu, oracle, table):
     for n in (0, 1, 63, 64, 1023, 1024, 1025, 4095, 4096, 4097):
         from bs_amd.synth import splitmix_bytes
