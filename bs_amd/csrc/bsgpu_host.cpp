@@ -720,14 +720,11 @@ struct bsg_ctx {
 
   int close() {
     if (fill == 0 && pos == 0) return BSG_OK;  // empty stream: no chunks
-    // (a stream that ends exactly at a tile boundary flushes its open chunk with an empty
-    // final segment)
-    int rc = reclaim(cur);
-    if (rc) return rc;
-    if (fill == 0) {
-      HCHECK(slots[cur].staging.ensure(16));
-    }
-    rc = submit(true);
+    // The final segment must hold at least one byte: the open chunk's flush is emitted by the
+    // scan of its last strip. write() and window() never submit a tile without leaving bytes
+    // behind, so this cannot happen; fail loudly rather than drop the last chunk.
+    if (fill == 0) return BSG_ESTATE;
+    int rc = submit(true);
     if (rc) return rc;
     while (!inflight.empty()) {
       bool got = false;
