@@ -132,7 +132,11 @@ __device__ __forceinline__ void slow_block(const ScanArgs& a, const uint32_t* ta
 // folds to a constant.
 typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
 __device__ __forceinline__ uint32_t lds_at(const uint32_t*, uint32_t byte_addr) {
+#ifdef BSG_SCAN_NOLDS  // experiment builds only: no table lookups (results meaningless)
+  return byte_addr * 0x9E3779B1u;
+#else
   return *reinterpret_cast<lds_u32p>(static_cast<uintptr_t>(byte_addr));
+#endif
 }
 __device__ __forceinline__ bool table_at_lds0(const uint32_t* tab) {
   return (uint32_t)(uintptr_t)((lds_u32p)tab) == 0u;
