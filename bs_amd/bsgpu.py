@@ -110,6 +110,9 @@ def lib() -> ctypes.CDLL:
         "bsg_store_put": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp,
                                          ctypes.POINTER(ctypes.c_int)]),
         "bsg_store_list": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
+        "bsg_store_put_ref": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_int)]),
+        "bsg_store_list_from": (ctypes.c_size_t, [vp, vp, vp, ctypes.c_size_t]),
         "bsg_writer_new": (vp, [ctypes.c_int, vp, ctypes.POINTER(Params), ctypes.c_size_t,
                                 ctypes.POINTER(ctypes.c_int)]),
         "bsg_writer_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
@@ -445,6 +448,21 @@ class MemStore:
         b = bytes(blob)
         _check(lib().bsg_store_put(self.h, b, len(b), ref, ctypes.byref(added)), "put")
         return ref.raw, bool(added.value)
+
+    def put_ref(self, ref: bytes, blob: bytes) -> bool:
+        """PutWithRef: store blob under a ref the caller computed (no hashing)."""
+        added = ctypes.c_int(0)
+        b = bytes(blob)
+        _check(lib().bsg_store_put_ref(self.h, bytes(ref), b, len(b), ctypes.byref(added)),
+               "put_ref")
+        return bool(added.value)
+
+    def refs_after(self, start: bytes) -> list[bytes]:
+        """ListRefs(start, ...): refs > start, lexicographic."""
+        n = lib().bsg_store_list_from(self.h, bytes(start), None, 0)
+        buf = ctypes.create_string_buffer(32 * max(n, 1))
+        lib().bsg_store_list_from(self.h, bytes(start), buf, n)
+        return [buf.raw[32 * i:32 * i + 32] for i in range(n)]
 
     def get(self, ref: bytes) -> bytes:
         n = ctypes.c_size_t(0)

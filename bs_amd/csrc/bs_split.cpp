@@ -683,6 +683,34 @@ int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[3
   return BSG_OK;
 }
 
+int bsg_store_put_ref(bsg_store* s, const uint8_t ref[32], const uint8_t* data, size_t n,
+                      int* added) {
+  if (!s || !ref || (!data && n)) return BSG_EINVAL;
+  auto* rp = dynamic_cast<bs::RefPutter*>(s->st.get());
+  if (!rp) return BSG_EINVAL;
+  bs::Ref r;
+  std::memcpy(r.data(), ref, 32);
+  bool a = false;
+  static const uint8_t empty = 0;
+  bs::Status st = rp->PutWithRef(r, n ? data : &empty, n, &a);
+  if (!st.ok()) return st.code;
+  if (added) *added = a ? 1 : 0;
+  return BSG_OK;
+}
+
+size_t bsg_store_list_from(bsg_store* s, const uint8_t start[32], uint8_t* refs, size_t cap) {
+  if (!s || !start) return 0;
+  bs::Ref st;
+  std::memcpy(st.data(), start, 32);
+  size_t k = 0;
+  s->st->ListRefs(st, [&](const bs::Ref& r) {
+    if (k < cap && refs) std::memcpy(refs + 32 * k, r.data(), 32);
+    ++k;
+    return bs::Status::Ok();
+  });
+  return k;
+}
+
 size_t bsg_store_list(bsg_store* s, uint8_t* refs, size_t cap) {
   if (!s) return 0;
   size_t k = 0;

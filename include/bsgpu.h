@@ -175,6 +175,13 @@ size_t bsg_store_count(const bsg_store* s);
 /* Get: copies min(cap, len) bytes, *n = blob length; returns BSG_ENOTFOUND if absent. */
 int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n);
 int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[32], int* added);
+/* Put with a ref the caller already has (a chunk record's ref): no hash is computed, the store
+ * trusts the ref (bs::RefPutter in bs_split.hpp). Needs no GPU. */
+int bsg_store_put_ref(bsg_store* s, const uint8_t ref[32], const uint8_t* data, size_t n,
+                      int* added);
+/* ListRefs(start, f) (store.go:13-24; mem.go:39-59, file.go:83-160): refs > start in lexicographic order, up to cap of them
+ * into refs (32 bytes each); returns the total count after start. */
+size_t bsg_store_list_from(bsg_store* s, const uint8_t start[32], uint8_t* refs, size_t cap);
 /* All refs in lexicographic order (32 bytes each, up to cap); returns the total count. */
 size_t bsg_store_list(bsg_store* s, uint8_t* refs, size_t cap);
 
