@@ -23,6 +23,15 @@
 // Wave-mode rounds: 1 (default) = skewed lane pairs, 9 VALU per round (sha256_rounds_skew,
 // 2,941 cycles per block on MI355X; the banked pair of sha256_rounds_bank takes 3,161); 0 = one
 // lane runs the whole round, 14 VALU (4,021 cycles). tools/ubench/skew.hip measures all three.
+// k_scan block loop: 1 = words loaded two blocks ahead of their table lookups, 0 = one ahead.
+// k_scan: pin the order of LDS lookups and hash steps (sched_group_barrier), 1 lookup per 4 ALU.
+#ifndef BSG_SCAN_SCHED
+#define BSG_SCAN_SCHED 0
+#endif
+#ifndef BSG_SCAN_AHEAD2
+#define BSG_SCAN_AHEAD2 0
+#endif
+
 #ifndef BSG_BANK_ROUNDS
 #define BSG_BANK_ROUNDS 1
 #endif
@@ -34,8 +43,13 @@ typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(16)));
 
 __device__ __forceinline__ uint32_t tz32(uint32_t h) { return h ? (uint32_t)__builtin_ctz(h) : 32u; }
 
+typedef const __attribute__((address_space(1))) u32x4* g_u32x4p;
+
+// All stream data is in device global memory; the explicit address space keeps these global
+// loads (vmcnt only) even where hipcc cannot infer it (e.g. after ScanArgs went through a call),
+// instead of flat loads that also count against lgkmcnt, the LDS lookups' counter.
 __device__ __forceinline__ void load16(const uint8_t* p, uint32_t (&w)[16]) {
-  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  g_u32x4p q = (g_u32x4p)(p);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     u32x4 v = q[i];
@@ -108,15 +122,22 @@ __device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t st
   c.count++;
 }
 
+// Exact re-scan of one 64-byte block whose pre-filter hit. The hash at the block start is
+// rebuilt from the 64 bytes before it (the window property: h depends only on those bytes), so
+// the fast loop keeps no state for it, just one bit per block. noinline: its registers stay out
+// of the fast loop's allocation (an inlined re-scan made hipcc spill the fast loop's history).
 template <bool WRITE>
-__device__ __forceinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
+__device__ __noinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
                                         const uint8_t* d, const StreamDesc* sd, StripCtx& c,
-                                        uint64_t strip, uint64_t off, uint32_t h) {
+                                        uint64_t strip, uint64_t off) {
   uint32_t w[16], pw[16];
   load16(d + off, w);
   if (off >= 64) load16(d + off - 64, pw);
   else load16(sd->hist, pw);
   const uint32_t mask = a.p.mask;
+  uint32_t h = 0;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) h = rotl1(h) ^ lookup(tab, pw[k >> 2], lane4, k);
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
     uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
@@ -169,6 +190,14 @@ __device__ __forceinline__ bool chain64(const uint32_t* tab, const uint32_t (&wn
       }
       const uint32_t pk = __builtin_amdgcn_perm(h, h0, 0x05040100u);  // lo16(h0) | lo16(h)<<16
       m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, pk));
+#if BSG_SCAN_SCHED
+      if (LOAD) {  // interleave: one LDS lookup per byte between the hash steps
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0001, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x0001, 4, 0);
+      }
+#endif
     }
     return m.x == 0 || m.y == 0;
   } else {
@@ -201,43 +230,86 @@ __device__ __forceinline__ void scan_load16(const uint8_t* p, uint32_t (&w)[16])
 #endif
 }
 
+template <int N>
+__device__ __forceinline__ void hit_mark(uint32_t (&hits)[N], uint32_t b, bool hit) {
+  if (N == 1) {
+    hits[0] |= hit ? 1u << b : 0u;
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) hits[i] |= (hit && (b >> 5) == (uint32_t)i) ? 1u << (b & 31) : 0u;
+  }
+}
+
 // All full 64-byte blocks of a strip. On entry hA = table values of the 64 bytes before the
-// strip and h = the hash there; on exit hA = those of the last full block.
+// strip and h = the hash there; on exit hA = those of the last full block. Blocks whose
+// pre-filter hits are only marked here (one bit each in kHitWords words) and re-scanned
+// exactly afterwards in block order, so the candidate order is unchanged and the loop holds
+// nothing but the two histories, two word blocks and the hash.
 template <bool WRITE, bool WIDE>
 __device__ __forceinline__ void scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
                                                  uint32_t lane4, const uint8_t* d,
                                                  const StreamDesc* sd, StripCtx& c, uint64_t strip,
                                                  uint32_t nfull, uint32_t& h, uint32_t (&hA)[64]) {
+  constexpr int kHitWords = (kStrip / 64 + 31) / 32;
   const uint32_t mask = a.p.mask;
   const uint8_t* base = d + c.start;
   uint32_t hB[64];
   uint32_t w[16], wn[16];
+  uint32_t hits[kHitWords];
+#pragma unroll
+  for (int i = 0; i < kHitWords; ++i) hits[i] = 0;
   scan_load16(base, w);
   lookup64(tab, w, hB, lane4);                       // hB = block 0
-  scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
   uint32_t b = 0;
+#if BSG_SCAN_AHEAD2
+  // Four blocks per iteration with the words loaded two blocks ahead of their lookups (p: the
+  // next two blocks, q: the two after), so a block's loads have two blocks of hashing to land.
+  if (nfull >= 4) {
+    uint32_t p0[16], p1[16], q0[16], q1[16];
+    scan_load16(base + 64, p0);
+    scan_load16(base + 128, p1);
+    for (; b + 3 < nfull; b += 4) {
+      scan_load16(base + 64ull * (b + 3), q0);
+      scan_load16(base + 64ull * min(b + 4, nfull - 1), q1);
+      hit_mark(hits, b, chain64<WIDE, true>(tab, p0, hA, hB, h, lane4, mask));
+      hit_mark(hits, b + 1, chain64<WIDE, true>(tab, p1, hB, hA, h, lane4, mask));
+      scan_load16(base + 64ull * min(b + 5, nfull - 1), p0);
+      scan_load16(base + 64ull * min(b + 6, nfull - 1), p1);
+      hit_mark(hits, b + 2, chain64<WIDE, true>(tab, q0, hA, hB, h, lane4, mask));
+      hit_mark(hits, b + 3, chain64<WIDE, true>(tab, q1, hB, hA, h, lane4, mask));
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = p0[i];  // block b+1 for the remainder below
+  } else {
+    scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
+  }
+#else
+  scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
+#endif
   for (; b + 1 < nfull; b += 2) {
     // block b: out-going hA, in-coming hB; looks up block b+1 into hA
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = wn[i];
     scan_load16(base + 64ull * min(b + 2, nfull - 1), wn);
-    uint32_t h0 = h;
-    if (__builtin_expect(chain64<WIDE, true>(tab, w, hA, hB, h, lane4, mask), 0))
-      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * b, h0);
+    hit_mark(hits, b, chain64<WIDE, true>(tab, w, hA, hB, h, lane4, mask));
     // block b+1: out-going hB, in-coming hA; looks up block b+2 into hB
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = wn[i];
     scan_load16(base + 64ull * min(b + 3, nfull - 1), wn);
-    h0 = h;
-    if (__builtin_expect(chain64<WIDE, true>(tab, w, hB, hA, h, lane4, mask), 0))
-      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * (b + 1), h0);
+    hit_mark(hits, b + 1, chain64<WIDE, true>(tab, w, hB, hA, h, lane4, mask));
   }
   if (b < nfull) {  // odd block count: the last block, then its values back into hA
-    const uint32_t h0 = h;
-    if (__builtin_expect(chain64<WIDE, false>(tab, w, hA, hB, h, lane4, mask), 0))
-      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * b, h0);
+    hit_mark(hits, b, chain64<WIDE, false>(tab, w, hA, hB, h, lane4, mask));
 #pragma unroll
     for (int k = 0; k < 64; ++k) hA[k] = hB[k];
+  }
+#pragma unroll
+  for (int i = 0; i < kHitWords; ++i) {
+    while (hits[i]) {
+      const uint32_t bb = 32u * i + (uint32_t)__builtin_ctz(hits[i]);
+      hits[i] &= hits[i] - 1;
+      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * bb);
+    }
   }
 }
 
