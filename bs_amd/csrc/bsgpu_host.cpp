@@ -81,6 +81,18 @@ struct PinBuf {
     cap = bytes;
     return hipSuccess;
   }
+  // ensure() that keeps the first `keep` bytes
+  hipError_t grow(size_t bytes, size_t keep) {
+    if (bytes <= cap) return hipSuccess;
+    void* q = nullptr;
+    hipError_t e = hipHostMalloc(&q, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    if (keep) std::memcpy(q, p, keep);
+    if (p) hipHostFree(p);
+    p = q;
+    cap = bytes;
+    return hipSuccess;
+  }
   void release() {
     if (p) hipHostFree(p);
     p = nullptr;
@@ -621,6 +633,19 @@ struct bsg_ctx {
     return BSG_OK;
   }
 
+  // Pinned staging grows with the stream's first tile (doubling from 4 MiB up to the tile), so
+  // a small stream pins a few MiB, not a whole tile: pinning 256 MiB took ~50 ms, most of a
+  // small Write.
+  static constexpr size_t kMinStaging = 4ull << 20;
+  int grow_staging(TileSlot& t, size_t need) {
+    if (need <= t.staging.cap) return BSG_OK;
+    // past its first tile a stream is a big one: later tiles get the whole tile at once
+    const size_t nc = pos > 0 ? tile
+                              : std::min(tile, std::max({need, 2 * t.staging.cap, kMinStaging}));
+    HCHECK(t.staging.grow(nc, fill));
+    return BSG_OK;
+  }
+
   // Host side of Write: bytes into the current slot's pinned staging (large pieces on several
   // threads), submitting full tiles as more data arrives.
   int write(const uint8_t* p, size_t n) {
@@ -633,10 +658,11 @@ struct bsg_ctx {
       if (fill == 0) {
         // the staging buffer is free once its last H2D has run; the slot's engine and device
         // buffer are reclaimed only at submit(), so the host copy overlaps that tile's k_sha
-        HCHECK(t.staging.ensure(tile));
         HCHECK(hipEventSynchronize(t.h2d_ev));
       }
       const size_t k = std::min(n, tile - fill);
+      int rc = grow_staging(t, fill + k);
+      if (rc) return rc;
       par_copy(t.staging.as<uint8_t>() + fill, p, k);
       fill += k;
       p += k;
@@ -661,22 +687,23 @@ struct bsg_ctx {
       int rc = submit(false);
       if (rc) return rc;
       TileSlot& n = slots[cur];
-      HCHECK(n.staging.ensure(tile));
       HCHECK(hipEventSynchronize(n.h2d_ev));
+      int rc2 = grow_staging(n, hold);  // (fill is 0 here: nothing to keep)
+      if (rc2) return rc2;
       std::memcpy(n.staging.p, held, hold);
       fill = hold;
     }
     TileSlot& t = slots[cur];
-    if (fill == 0) {
-      HCHECK(t.staging.ensure(tile));
-      HCHECK(hipEventSynchronize(t.h2d_ev));
-    }
+    if (fill == 0) HCHECK(hipEventSynchronize(t.h2d_ev));
+    // the window is the staging buffer's free part; a full one grows (keeping what it holds)
+    int rc = grow_staging(t, fill + 1);
+    if (rc) return rc;
     *p = t.staging.as<uint8_t>() + fill;
-    *cap = tile - fill;
+    *cap = std::min(t.staging.cap, tile) - fill;
     return BSG_OK;
   }
   int commit(size_t n) {
-    if (n > tile - fill) return BSG_EINVAL;
+    if (n > std::min(slots[cur].staging.cap, tile) - fill) return BSG_EINVAL;
     fill += n;
     return poll();
   }

@@ -76,9 +76,11 @@ bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table /*
 /* Copies p[0..n) into pinned staging (the caller keeps ownership of p); full tiles are split
  * and hashed on the device as they fill. */
 int bsg_write(bsg_ctx* ctx, const uint8_t* p, size_t n);
-/* Zero-copy Write: *p / *cap = the free rest of the current pinned staging tile; the caller
- * fills up to *cap bytes there (e.g. an io.Reader reads straight into it) and commits n of
- * them. Same stream semantics as bsg_write; the window is valid until the next call on ctx. */
+/* Zero-copy Write: *p / *cap = the free rest of the current pinned staging buffer (never more
+ * than the rest of the tile; the buffer grows from 4 MiB to the tile size as the stream does,
+ * so early windows are smaller); the caller fills up to *cap bytes there (e.g. an io.Reader
+ * reads straight into it) and commits n of them. Same stream semantics as bsg_write; the
+ * window is valid until the next call on ctx. */
 int bsg_write_window(bsg_ctx* ctx, uint8_t** p, size_t* cap);
 int bsg_write_commit(bsg_ctx* ctx, size_t n);
 /* Flushes the final chunk (hashsplit Splitter.Close). Idempotent. */
