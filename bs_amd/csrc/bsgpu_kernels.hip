@@ -83,8 +83,8 @@ __device__ __forceinline__ void load_table(uint32_t* tab, const uint32_t* __rest
   }
 }
 
-__device__ __forceinline__ uint32_t find_stream(const uint64_t* __restrict__ strip0, uint32_t n,
-                                                uint64_t strip) {
+template <class P>
+__device__ __forceinline__ uint32_t find_stream(P strip0, uint32_t n, uint64_t strip) {
   // largest s in [0, n) with strip0[s] <= strip (zero-length streams are skipped)
   uint32_t lo = 0, hi = n;  // invariant: strip0[lo] <= strip < strip0[hi]
   while (hi - lo > 1) {
@@ -313,14 +313,33 @@ __device__ __forceinline__ void scan_full_blocks(const ScanArgs& a, const uint32
   }
 }
 
+// strip0 (the streams' first strips) cached in LDS after the table, when it fits: the stream
+// of a strip is a binary search over it, one dependent load per step, at every strip start.
+constexpr uint32_t kStrip0Lds = 2048;
+typedef const __attribute__((address_space(3))) uint64_t* lds_u64p;
+
+__device__ __forceinline__ lds_u64p cache_strip0(uint32_t* lds_after, const ScanArgs& a) {
+  if (a.nstreams + 1 > kStrip0Lds) return nullptr;
+  uint64_t* s0 = reinterpret_cast<uint64_t*>(lds_after);
+  for (uint32_t i = threadIdx.x; i <= a.nstreams; i += blockDim.x) s0[i] = a.strip0[i];
+  return (lds_u64p)(s0);  // generic -> LDS address space
+}
+
 template <bool WRITE>
 __device__ __forceinline__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                               uint64_t strip, uint64_t wbase) {
+                               uint64_t strip, uint64_t wbase, lds_u64p s0 = nullptr) {
   StripCtx c;
-  c.stream = find_stream(a.strip0, a.nstreams, strip);
+  uint64_t first;
+  if (s0) {
+    c.stream = find_stream(s0, a.nstreams, strip);
+    first = s0[c.stream];
+  } else {
+    c.stream = find_stream(a.strip0, a.nstreams, strip);
+    first = a.strip0[c.stream];
+  }
   const StreamDesc* sd = a.streams + c.stream;
   const uint64_t seglen = sd->len;
-  c.start = (strip - sd->strip0) * (uint64_t)kStrip;
+  c.start = (strip - first) * (uint64_t)kStrip;
   c.count = 0;
   c.wbase = wbase;
   c.seg_base = sd->seg_base;
@@ -374,47 +393,66 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
     return;
   }
   load_table(tab, a.table);
+  const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
     if (strip < a.nstrips) {
-      const uint32_t n = scan_strip<false>(a, tab, lane4, strip, 0);
+      const uint32_t n = scan_strip<false>(a, tab, lane4, strip, 0, s0);
       a.counts[strip] = n;
       if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
     }
   }
 }
 
-__global__ __launch_bounds__(kScanWG, 2) void k_compact(ScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+// Slots -> the sorted candidate list, one lane per strip. No table and no re-scan registers,
+// so many waves per SIMD hide the loads; strips whose candidates overflowed their slots are
+// left to k_rescan.
+__global__ __launch_bounds__(256) void k_compact(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (a.ctr->overflow) return;
+  const lds_u64p s0 = cache_strip0(lds, a);
+  __syncthreads();
+  for (uint64_t strip = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; strip < a.nstrips;
+       strip += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t cnt = a.counts[strip];
+    if (cnt == 0 || cnt > (uint32_t)kSlotCap) continue;
+    const uint64_t base = a.cand_off[strip];
+    uint32_t st;
+    uint64_t first;
+    if (s0) {
+      st = find_stream(s0, a.nstreams, strip);
+      first = s0[st];
+    } else {
+      st = find_stream(a.strip0, a.nstreams, strip);
+      first = a.strip0[st];
+    }
+    const uint64_t start = a.streams[st].seg_base + (strip - first) * (uint64_t)kStrip;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint32_t v = a.slots[strip * kSlotCap + i];
+      if (base + i < a.cand_cap)
+        a.cand[base + i] = cand_pack(st, start + (v >> 8), (v & 0x80u) != 0, v & 63u);
+    }
+  }
+}
+
+// Strips with more candidates than slots (k_scan counted them in ctr->rescan) are scanned
+// again, writing straight into the candidate list. Exits at once when there are none.
+__global__ __launch_bounds__(kScanWG, 2) void k_rescan(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+  if (a.ctr->overflow || !a.ctr->rescan) return;
   if (!table_at_lds0(tab)) {
     if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
     return;
   }
-  if (a.ctr->rescan) {  // uniform: some strip overflowed its slots, re-scans need the table
-    load_table(tab, a.table);
-    __syncthreads();
-  }
+  load_table(tab, a.table);
+  __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
     const uint32_t cnt = strip < a.nstrips ? a.counts[strip] : 0u;
-    if (cnt == 0) continue;
-    const uint64_t base = a.cand_off[strip];
-    if (cnt <= (uint32_t)kSlotCap) {
-      const uint32_t s = find_stream(a.strip0, a.nstreams, strip);
-      const StreamDesc* sd = a.streams + s;
-      const uint64_t start = sd->seg_base + (strip - sd->strip0) * (uint64_t)kStrip;
-      for (uint32_t i = 0; i < cnt; ++i) {
-        const uint32_t v = a.slots[strip * kSlotCap + i];
-        if (base + i < a.cand_cap)
-          a.cand[base + i] = cand_pack(s, start + (v >> 8), (v & 0x80u) != 0, v & 63u);
-      }
-    } else {
-      scan_strip<true>(a, tab, lane4, strip, base);
-    }
+    if (cnt > (uint32_t)kSlotCap) scan_strip<true>(a, tab, lane4, strip, a.cand_off[strip]);
   }
 }
 
@@ -1255,14 +1293,16 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
   const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
   const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_scan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
+  hipLaunchKernelGGL(k_scan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus) {
   const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
   const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_compact, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
+  const uint32_t cgrid = grid_for(a.nstrips, 256, 16u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_compact, dim3(cgrid), dim3(256), kStrip0Lds * 8, s, a);
+  hipLaunchKernelGGL(k_rescan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
   return hipGetLastError();
 }
 

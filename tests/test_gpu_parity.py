@@ -113,6 +113,25 @@ def test_multistream_random_vs_oracle(gpu, oracle, table, bits, min_size):
     assert k == len(ch)
 
 
+def test_many_streams_past_lds_cache(gpu, oracle, table):
+    """3,000 streams: more than the 2,047 whose first strips k_scan / k_compact cache in LDS, so
+    the stream of a strip is searched in global memory; short, empty and multi-strip streams."""
+    from bs_amd.synth import splitmix_array
+    rng = np.random.default_rng(3000)
+    lens = [int(x) for x in rng.integers(0, 9000, size=3000)]
+    lens[5] = 0
+    lens[2500] = 70_000
+    arrs = [splitmix_array(5000 + i, n) for i, n in enumerate(lens)]
+    ch, counts = gpu.split_hash_batch(arrs, bits=12, min_size=64)
+    k = 0
+    for i, a in enumerate(arrs):
+        one = oracle.split(table, a, bits=12, min_size=64)
+        got = ch[k:k + int(counts[i])]
+        assert as_tuples(got) == as_tuples(one), (i, len(a))
+        k += int(counts[i])
+    assert k == len(ch)
+
+
 def test_dense_candidates_zero_runs(gpu, oracle, table):
     """Long zero runs inside random data: every position in the run is a candidate."""
     from bs_amd.synth import splitmix_array
