@@ -274,12 +274,19 @@ for idx, (name, f) in enumerate(PATS):
             '    "' + "\\n".join(body) + '\\n"',
             '    "s_sub_u32 s12, s12, 1\\n s_cmp_lg_u32 s12, 0\\n s_cbranch_scc1 .Lloop%=\\n"',
             '    :: "s"(iters) : "s8", "s10", "s11", "s12", "scc", ' + ", ".join(f'"v{r}"' for r in range(40, 72)) + ');',
+            '  __syncthreads();',
             '  STAMP(t1);',
             '  }',
             f'  if (threadIdx.x == 0) {{ out[0] = t1 - t0; out[1] = {len(body)}; }}',
             '}', '']
 src += ['int main() {', '  uint64_t* d; (void)hipMalloc(&d, 16); uint64_t h[2]; const int iters = 400;']
+MULTI = {"add3 3 vgpr", "add VOP2", "skew round, 1 chain", "bitop3 3 vgpr"}
 for idx, (name, f) in enumerate(PATS):
+    if name in MULTI:
+        for w in (1, 2, 4):
+            src += [f'  hipLaunchKernelGGL(k{idx}, dim3(1), dim3({256 * w}), 0, 0, d, iters); (void)hipDeviceSynchronize();',
+                    '  (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);',
+                    f'  printf("%-44s {w} waves/SIMD: %.2f cycles per instr per SIMD\\n", "{name}", (double)h[0] / ((double)iters * h[1] * {w}));']
     src += [f'  hipLaunchKernelGGL(k{idx}, dim3(1), dim3(64), 0, 0, d, iters); (void)hipDeviceSynchronize();',
             '  (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);',
             f'  printf("%-44s %.2f cycles/instr  %u instrs\\n", "{name}", (double)h[0] / ((double)iters * h[1]), (unsigned)h[1]);']
