@@ -90,6 +90,7 @@ def lib() -> ctypes.CDLL:
         "bsg_engine_candidates": (ctypes.c_uint64, [vp]),
         "bsg_engine_profile": (ctypes.c_int, [vp, ctypes.c_int]),
         "bsg_engine_diag": (ctypes.c_int, [vp, u64p]),
+        "bsg_engine_timeline": (ctypes.c_int, [vp, u64p]),
         "bsg_engine_stage_ms": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float)]),
         "bsg_split_hash_batch": (ctypes.c_int, [ctypes.c_int, vp, u64p, u64p, ctypes.c_uint32,
                                                 ctypes.POINTER(Params), u32p, vp,
@@ -312,6 +313,12 @@ class Engine:
         _check(lib().bsg_engine_diag(self.h, _p(d, ctypes.c_uint64)), "bsg_engine_diag")
         out = {"nlong": int(d[0]), "long_thresh": int(d[1]), "max_nblocks": int(d[2]),
                "nshort": int(d[13]), "wave_tickets": int(d[14]), "total_blocks": int(d[15])}
+        t = np.zeros(4, dtype=np.uint64)
+        _check(lib().bsg_engine_timeline(self.h, _p(t, ctypes.c_uint64)), "bsg_engine_timeline")
+        if t[0] and t[1] and t[3]:  # microseconds after the first k_sha wave started
+            out["timeline_us"] = {"long_start": round(float(t[1] - t[0]) * 0.01, 1),
+                                  "long_end": round(float(t[2] - t[0]) * 0.01, 1),
+                                  "lane_end": round(float(t[3] - t[0]) * 0.01, 1)}
         for tag, o in (("long", 3), ("lane", 8)):
             cyc, rt, nb = int(d[o + 1] - d[o]), int(d[o + 3] - d[o + 2]), int(d[o + 4])
             if nb and rt:

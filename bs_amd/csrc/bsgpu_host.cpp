@@ -960,6 +960,15 @@ int bsg_engine_diag(const bsg_engine* e, uint64_t out[16]) {
   return BSG_OK;
 }
 
+int bsg_engine_timeline(const bsg_engine* e, uint64_t out[4]) {
+  if (!e || !out) return BSG_EINVAL;
+  out[0] = e->last.sha_start_rt;
+  out[1] = e->last.diag[2];  // longest wave-mode job: start, end
+  out[2] = e->last.diag[3];
+  out[3] = e->last.lane_end_rt;
+  return BSG_OK;
+}
+
 bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, int* err) {
   int dummy;
   if (!err) err = &dummy;

@@ -103,7 +103,10 @@ struct Counters {
   uint64_t total_blocks;       // SHA-256 blocks over all jobs (k_lens)
   uint64_t long_buckets;       // LPT buckets [0, long_buckets) of wave-eligible jobs -> wave mode
   uint64_t ntickets;           // wave-mode work items: kSolo single jobs, then groups of kGroup
-  uint64_t pad_[7];
+  uint64_t sha_arrivals;       // k_sha waves started (diagnostic)
+  uint64_t sha_start_rt;       // s_memrealtime of the first k_sha wave (diagnostic)
+  uint64_t lane_end_rt;        // latest s_memrealtime at which a wave left per-lane mode
+  uint64_t pad_[4];
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 

@@ -24,6 +24,11 @@
 // 2,941 cycles per block on MI355X; the banked pair of sha256_rounds_bank takes 3,161); 0 = one
 // lane runs the whole round, 14 VALU (4,021 cycles). tools/ubench/skew.hip measures all three.
 // k_scan block loop: 1 = words loaded two blocks ahead of their table lookups, 0 = one ahead.
+// Wave-mode threshold: jobs of at least this percentage of the longest job's blocks run on
+// skewed lane pairs (see k_bucket_scan).
+#ifndef BSG_TLEN_PCT
+#define BSG_TLEN_PCT 43
+#endif
 // k_scan: pin the order of LDS lookups and hash steps (sched_group_barrier), 1 lookup per 4 ALU.
 #ifndef BSG_SCAN_SCHED
 #define BSG_SCAN_SCHED 0
@@ -957,7 +962,7 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   const uint32_t t = threadIdx.x;
   if (t == 0) nok = 0;
   const uint64_t mx = a.ctr->max_nblocks, w = a.ctr->bucket_width;
-  uint64_t tlen = (mx * 43) / 100;
+  uint64_t tlen = (mx * BSG_TLEN_PCT) / 100;
   const uint64_t share = (a.ctr->total_blocks * 9) / (10ull * 64ull * a.waves);
   tlen = max(max(tlen, share), (uint64_t)kLongMinBlocks);
   uint64_t cap = kSolo + (uint64_t)kGroup * (a.waves / 2 > kSolo ? a.waves / 2 - kSolo : 0);
@@ -1187,19 +1192,40 @@ __device__ __forceinline__ uint64_t pop_uniform(uint64_t* head) {
 // wave-instruction; a second wave on the SIMD only runs in the first one's gaps), so stacking
 // waves gains nothing and would stall the latency-critical wave-mode chains. Every wave first
 // drains the long-job queue in wave mode, then turns to per-lane mode (longest-first order).
-__global__ __launch_bounds__(256, 1) void k_sha(ShaArgs a) {
+#ifndef BSG_SHA_WAVES
+#define BSG_SHA_WAVES 4
+#endif
+constexpr uint32_t kShaWaves = BSG_SHA_WAVES;
+static_assert(kShaWaves == 4 || kShaWaves == 8, "4 chain-capable waves per workgroup (+4 lane-only)");
+
+__global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (a.ctr->overflow || a.ctr->error) return;
   const uint64_t M = a.ctr->nchunks;
   if (M > a.chunk_cap) return;  // k_chunks flagged the error
   const uint64_t nlong = a.ctr->nlong;
-  uint32_t* ring = lds + (threadIdx.x >> 6) * kRingWords;
-  // row of ones after each wave's 64 K+W rows (the A lanes' kw in sha256_rounds_bank)
-  for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 1u;
-  // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
-  // break; }` form was restructured by hipcc into a nested loop that re-entered job 0 forever.
+  if ((threadIdx.x & 63u) == 0) {  // diagnostic timeline: when the kernel's first wave started
+    const uint64_t rt = __builtin_amdgcn_s_memrealtime();
+    if (atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->sha_arrivals), 1ull) == 0)
+      a.ctr->sha_start_rt = rt;
+  }
   const uint64_t ntickets = a.ctr->ntickets;
-  uint64_t t = pop_uniform(&a.ctr->long_head);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // BSG_SHA_WAVES=8 (experiment): the first ceil(tickets / 4) workgroups take
+  // the wave-mode tickets on waves 0-3 (waves 4-7 leave at once, so no chain shares its SIMD);
+  // every other workgroup runs per-lane mode on all 8 waves, two per SIMD. The chains kept
+  // their speed, but the longest per-lane jobs, now sharing a SIMD, took 1.5x as long.
+  const bool chain_wg = kShaWaves == 4 || (uint64_t)blockIdx.x * 4 < ntickets;
+  if (kShaWaves > 4 && chain_wg && wv >= 4) return;
+  uint32_t* ring = lds + (wv & 3u) * kRingWords;
+  uint64_t t = ~0ull;
+  if (chain_wg) {
+    // row of ones after each wave's 64 K+W rows (the A lanes' kw in sha256_rounds_bank)
+    for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 1u;
+    // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
+    // break; }` form was restructured by hipcc into a nested loop that re-entered job 0 forever.
+    t = pop_uniform(&a.ctr->long_head);
+  }
   if (t < ntickets) {
     // A long chain is the launch's critical path. When another kernel's waves share its SIMD
     // (the streaming pipeline runs the next tile's scan beside this k_sha), the arbiter should
@@ -1212,6 +1238,9 @@ __global__ __launch_bounds__(256, 1) void k_sha(ShaArgs a) {
     __builtin_amdgcn_s_setprio(0);
   }
   sha_lane_mode(a, M);
+  if ((threadIdx.x & 63u) == 0)
+    atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->lane_end_rt),
+              (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1348,7 +1377,7 @@ static_assert(4 * kRingWords * 4 <= kShaLds, "wave rings fit");
 
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
   (void)job_bound;  // persistent: one workgroup per CU, waves loop over the job queues
-  hipLaunchKernelGGL(k_sha, dim3((uint32_t)num_cus), dim3(256), kShaLds, s, a);
+  hipLaunchKernelGGL(k_sha, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
   return hipGetLastError();
 }
 

@@ -133,6 +133,9 @@ int bsg_engine_stage_ms(const bsg_engine* eng, float out[3]);
  * start/end (100 MHz) and block count, [8..12] the same for the longest per-lane job,
  * [13] per-lane job count. */
 int bsg_engine_diag(const bsg_engine* eng, uint64_t out[16]);
+/* Diagnostic timeline of the last run's k_sha, in 100 MHz s_memrealtime ticks: first wave
+ * started, longest wave-mode job started / ended, last wave left per-lane mode. */
+int bsg_engine_timeline(const bsg_engine* eng, uint64_t out[4]);
 /* Last run's candidate count (diagnostics). */
 uint64_t bsg_engine_candidates(const bsg_engine* eng);
 
