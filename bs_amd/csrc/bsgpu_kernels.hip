@@ -23,22 +23,13 @@
 // Wave-mode rounds: 1 (default) = skewed lane pairs, 9 VALU per round (sha256_rounds_skew,
 // 2,941 cycles per block on MI355X; the banked pair of sha256_rounds_bank takes 3,161); 0 = one
 // lane runs the whole round, 14 VALU (4,021 cycles). tools/ubench/skew.hip measures all three.
-// k_scan block loop: 1 = words loaded two blocks ahead of their table lookups, 0 = one ahead.
-// Wave-mode threshold: jobs of at least this percentage of the longest job's blocks run on
-// skewed lane pairs (see k_bucket_scan).
-#ifndef BSG_TLEN_PCT
-#define BSG_TLEN_PCT 43
-#endif
-// k_scan: pin the order of LDS lookups and hash steps (sched_group_barrier), 1 lookup per 4 ALU.
-#ifndef BSG_SCAN_SCHED
-#define BSG_SCAN_SCHED 0
-#endif
-#ifndef BSG_SCAN_AHEAD2
-#define BSG_SCAN_AHEAD2 0
-#endif
-
 #ifndef BSG_BANK_ROUNDS
 #define BSG_BANK_ROUNDS 1
+#endif
+// Wave-mode threshold: jobs of at least this percentage of the longest job's blocks run on
+// skewed lane pairs (k_bucket_scan; 40 measured the same, 37 / 35 / 28 worse on configs[2]).
+#ifndef BSG_TLEN_PCT
+#define BSG_TLEN_PCT 43
 #endif
 
 namespace bsg {
@@ -195,14 +186,6 @@ __device__ __forceinline__ bool chain64(const uint32_t* tab, const uint32_t (&wn
       }
       const uint32_t pk = __builtin_amdgcn_perm(h, h0, 0x05040100u);  // lo16(h0) | lo16(h)<<16
       m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, pk));
-#if BSG_SCAN_SCHED
-      if (LOAD) {  // interleave: one LDS lookup per byte between the hash steps
-        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x0001, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x0001, 4, 0);
-      }
-#endif
     }
     return m.x == 0 || m.y == 0;
   } else {
@@ -266,31 +249,7 @@ __device__ __forceinline__ void scan_full_blocks(const ScanArgs& a, const uint32
   scan_load16(base, w);
   lookup64(tab, w, hB, lane4);                       // hB = block 0
   uint32_t b = 0;
-#if BSG_SCAN_AHEAD2
-  // Four blocks per iteration with the words loaded two blocks ahead of their lookups (p: the
-  // next two blocks, q: the two after), so a block's loads have two blocks of hashing to land.
-  if (nfull >= 4) {
-    uint32_t p0[16], p1[16], q0[16], q1[16];
-    scan_load16(base + 64, p0);
-    scan_load16(base + 128, p1);
-    for (; b + 3 < nfull; b += 4) {
-      scan_load16(base + 64ull * (b + 3), q0);
-      scan_load16(base + 64ull * min(b + 4, nfull - 1), q1);
-      hit_mark(hits, b, chain64<WIDE, true>(tab, p0, hA, hB, h, lane4, mask));
-      hit_mark(hits, b + 1, chain64<WIDE, true>(tab, p1, hB, hA, h, lane4, mask));
-      scan_load16(base + 64ull * min(b + 5, nfull - 1), p0);
-      scan_load16(base + 64ull * min(b + 6, nfull - 1), p1);
-      hit_mark(hits, b + 2, chain64<WIDE, true>(tab, q0, hA, hB, h, lane4, mask));
-      hit_mark(hits, b + 3, chain64<WIDE, true>(tab, q1, hB, hA, h, lane4, mask));
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) wn[i] = p0[i];  // block b+1 for the remainder below
-  } else {
-    scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
-  }
-#else
   scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
-#endif
   for (; b + 1 < nfull; b += 2) {
     // block b: out-going hA, in-coming hB; looks up block b+1 into hA
 #pragma unroll
