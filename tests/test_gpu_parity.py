@@ -305,3 +305,49 @@ def test_dedup_edited_streams(gpu, oracle, table):
     refs_b = [bytes(r) for r in ch[na:]["ref"]]
     shared = sum(r in refs_a for r in refs_b) / len(refs_b)
     assert shared > 0.75, shared
+
+
+# --------------------------------------------------------------------------------------------
+# Seeded fuzz: random params, stream shapes, tiles, carry caps and Write sizes
+# --------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(24))
+def test_streaming_fuzz_vs_oracle(gpu, oracle, table, seed):
+    """Each seed draws split params (bits 8..22, MinSize 64..8192), a stream of 0..2.5 MB with
+    optional zero / period-32 stretches (dense candidates, h = 0 windows), a tile size, a carry
+    cap (device bytes, midstate, or a mix) and a Write-size pattern, and compares every chunk
+    with the oracle; the batch API (split_hash_batch) must agree with the streaming one."""
+    from bs_amd.synth import splitmix_bytes
+    rng = np.random.default_rng(9000 + seed)
+    bits = int(rng.integers(8, 23))
+    mn = int(rng.choice([64, 100, 1024, 4096, 8192]))
+    n = (int(rng.choice([0, 1, 63, 64, 65, 1023, 1024, 1025])) if rng.random() < 0.2
+         else int(rng.integers(10_000, 2_500_000)))
+    data = bytearray(splitmix_bytes(777 + seed, n))
+    if n > 10_000 and rng.random() < 0.5:  # a zero stretch: a candidate at every position
+        s = int(rng.integers(0, n - 5000))
+        z = int(rng.integers(100, 5000))
+        data[s:s + z] = bytes(z)
+    if n > 10_000 and rng.random() < 0.5:  # a period-32 stretch: h = 0 once the window is in it
+        s = int(rng.integers(0, n - 4096))
+        unit = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        data[s:s + 4096] = unit * 128
+    data = bytes(data)
+    tile = int(rng.choice([4096, 10_000, 65536, 1 << 20, 3 << 20]))
+    carry_cap = [None, 0, int(rng.integers(1, 200_000))][int(rng.integers(0, 3))]
+    want = as_tuples(oracle.split(table, data, bits=bits, min_size=mn))
+    w = gpu.StreamingSplitter(bits=bits, min_size=mn, tile=tile, carry_cap=carry_cap)
+    pos, got = 0, []
+    sizes = [1, 3, 64, 1000, 4096, 65536, 250_000]
+    while pos < len(data):
+        k = int(rng.choice(sizes))
+        w.write(data[pos:pos + k])
+        pos += k
+        if rng.random() < 0.5:
+            got.append(w.drain())
+    w.close()
+    got.append(w.drain())
+    w.free()
+    ch = np.concatenate(got) if got else got
+    assert as_tuples(ch) == want, (seed, bits, mn, n, tile, carry_cap)
+    bch, _ = gpu.split_hash_batch([np.frombuffer(data, dtype=np.uint8)], bits=bits, min_size=mn)
+    assert as_tuples(bch) == want, (seed, "batch")
