@@ -106,13 +106,16 @@ struct Counters {
   uint64_t sha_arrivals;       // k_sha waves started (diagnostic)
   uint64_t sha_start_rt;       // s_memrealtime of the first k_sha wave (diagnostic)
   uint64_t lane_end_rt;        // latest s_memrealtime at which a wave left per-lane mode
-  uint64_t pad_[4];
+  uint64_t nlong_grp;          // long jobs on solo / kGroup tickets; the rest of the long list
+  uint64_t tickets_grp;        //   runs on pair tickets (kPairGroup jobs, one lane pair each)
+  uint64_t pad_[2];
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 
 constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave path below 64 KiB
 constexpr uint32_t kSolo = 8;    // wave mode: the kSolo longest jobs run one per wave,
 constexpr uint32_t kGroup = 8;   // the next ones kGroup per wave (one banked lane pair each)
+constexpr uint32_t kPairGroup = 32;  // then (optionally) 32 per wave, one lane pair each
 constexpr int kLongRow = 68;               // LDS words per K+W row (64 + pad: conflict-free b128)
 constexpr int kRingWords = 65 * kLongRow;  // per wave: 64 K+W rows + one row of ones
 constexpr int kLptBuckets = 4096;          // longest-first job order: counting sort on nblocks

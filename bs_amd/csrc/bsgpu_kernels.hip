@@ -26,10 +26,16 @@
 #ifndef BSG_BANK_ROUNDS
 #define BSG_BANK_ROUNDS 1
 #endif
-// Wave-mode threshold: jobs of at least this percentage of the longest job's blocks run on
-// skewed lane pairs (k_bucket_scan; 40 measured the same, 37 / 35 / 28 worse on configs[2]).
+// Wave-mode tiers (k_bucket_scan), in percent of the longest job's blocks: jobs of at least
+// BSG_TLEN_PCT run on solo / group tickets (8 jobs per wave), jobs of BSG_PAIR_PCT up to that
+// on pair tickets (32 per wave, one skewed lane pair each, ring fills every 2 blocks), the rest
+// per lane. Measured on configs[2]: 56 / 30 gives 761-767 GiB/s against
+// 669-719 for 43 / off (the round-1 setting); configs[1] is unchanged (84.2-84.6).
 #ifndef BSG_TLEN_PCT
-#define BSG_TLEN_PCT 43
+#define BSG_TLEN_PCT 56
+#endif
+#ifndef BSG_PAIR_PCT
+#define BSG_PAIR_PCT 30
 #endif
 
 namespace bsg {
@@ -940,10 +946,35 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   __syncthreads();
   atomicAdd(&nok, ok);  // monotone in b: the eligible buckets are a prefix
   __syncthreads();
-  const uint32_t nlb = nok;
+  const uint32_t nlb8 = nok;
   uint32_t lv[4], lo[4], sv[4], so[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) lv[i] = (4 * t + i < nlb) ? e[i] : 0u;
+  for (int i = 0; i < 4; ++i) lv[i] = (4 * t + i < nlb8) ? e[i] : 0u;
+  const uint32_t n8 = block_scan4(lv, lo, wsum);
+  const uint64_t t8 = n8 <= kSolo ? n8 : kSolo + (n8 - kSolo + kGroup - 1) / kGroup;
+  uint32_t nlb = nlb8;
+  if (BSG_PAIR_PCT > 0 && a.long_mode == 0) {
+    // the next buckets, down to BSG_PAIR_PCT % of the longest, on pair tickets within the
+    // remaining half-of-the-waves ticket budget
+    const uint64_t tlen2 = max((mx * BSG_PAIR_PCT) / 100, (uint64_t)kLongMinBlocks);
+    const uint64_t tb = a.waves / 2 > t8 ? a.waves / 2 - t8 : 0;
+    const uint64_t cap2 = tb * kPairGroup;
+    uint32_t ok2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t b = 4 * t + i;
+      const uint64_t top = mx > b * w ? mx - b * w : 0;
+      ok2 += (b >= nlb8 && top >= tlen2 && (uint64_t)pe[i] + e[i] - n8 <= cap2) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (t == 0) nok = 0;
+    __syncthreads();
+    atomicAdd(&nok, ok2);
+    __syncthreads();
+    nlb = nlb8 + nok;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lv[i] = (4 * t + i < nlb) ? e[i] : 0u;
+  }
   const uint32_t nlong = block_scan4(lv, lo, wsum);
 #pragma unroll
   for (int i = 0; i < 4; ++i) sv[i] = a.bucket_cnt[4 * t + i] - lv[i];
@@ -958,7 +989,9 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
     a.ctr->nlong = nlong;
     a.ctr->nshort = nshort;
     a.ctr->long_thresh = mx > (uint64_t)nlb * w ? mx - (uint64_t)nlb * w : 0;  // diagnostic
-    a.ctr->ntickets = nlong <= kSolo ? nlong : kSolo + (nlong - kSolo + kGroup - 1) / kGroup;
+    a.ctr->nlong_grp = n8;
+    a.ctr->tickets_grp = t8;
+    a.ctr->ntickets = t8 + (nlong - n8 + kPairGroup - 1) / kPairGroup;
   }
 }
 
@@ -1014,16 +1047,19 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t nlong,
                              uint32_t* ring) {
   const uint32_t lane = threadIdx.x & 63u;
-  const bool solo = t < kSolo;
-  const uint64_t j0 = solo ? t : kSolo + (t - kSolo) * kGroup;
-  const uint32_t G = solo ? 1u : kGroup;
+  const uint64_t n8 = a.ctr->nlong_grp, t8 = a.ctr->tickets_grp;
+  const bool pairs = t >= t8;                  // pair tickets follow the solo / group ones
+  const bool solo = !pairs && t < kSolo;
+  const uint64_t j0 = solo ? t : pairs ? n8 + (t - t8) * kPairGroup : kSolo + (t - kSolo) * kGroup;
+  const uint64_t jend = pairs ? nlong : n8;    // a group ticket never reaches into the pair jobs
+  const uint32_t G = solo ? 1u : pairs ? kPairGroup : kGroup;
   const uint32_t B = 64u / G;                  // blocks per chain per ring fill
   const uint32_t cA = lane / B;                // chain this lane expands (phase A)
-  const uint32_t cR = solo ? 0u : lane >> 3;   // chain this lane's pair runs (phase B)
+  const uint32_t cR = cA;                      // chain this lane's pair runs (phase B)
   // phase-A job
   ShaJob ja;
   uint32_t sta[8];
-  const bool va = j0 + cA < nlong && sha_setup(a, a.long_list[j0 + cA], M, ja, sta);
+  const bool va = j0 + cA < jend && sha_setup(a, a.long_list[j0 + cA], M, ja, sta);
   if (!va) {  // empty slot of the last group: expand readable bytes, never used
     ja.dbase = a.data;
     ja.L = 0;
@@ -1034,7 +1070,7 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   // phase-B job (also the one this lane's pair finishes)
   ShaJob jb;
   uint32_t st[8];
-  const bool vb = j0 + cR < nlong && sha_setup(a, a.long_list[j0 + cR], M, jb, st);
+  const bool vb = j0 + cR < jend && sha_setup(a, a.long_list[j0 + cR], M, jb, st);
   const uint32_t nb = vb ? jb.nblocks : 0u;
   uint64_t tm0 = 0, tr0 = 0;
   if (t == 0) {  // timing stamps of the longest job (read back as Counters::diag)
@@ -1112,8 +1148,8 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     ring_sync();
   }
 #if BSG_BANK_ROUNDS
-  // each lane collects its octet's first pair: H0..H3 from the A lane, H4..H7 from the E lane
-  const int pe = (int)(lane & ~7u), pa = (int)((lane & ~7u) | 1u);
+  // each lane collects its chain's first pair: H0..H3 from the A lane, H4..H7 from the E lane
+  const int pe = (int)(lane & ~(B - 1u)), pa = (int)((lane & ~(B - 1u)) | 1u);
 #pragma unroll
   for (int k = 0; k < 4; ++k) st[k] = (uint32_t)__shfl((int)hs[k], pa);
   st[6] = (uint32_t)__shfl((int)hs[0], pe);
@@ -1121,7 +1157,7 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   st[4] = (uint32_t)__shfl((int)hs[2], pe);
   st[5] = (uint32_t)__shfl((int)hs[3], pe);
 #endif
-  if (vb && (lane & 7u) == 0 && (!solo || lane == 0)) {
+  if (vb && (lane & (B - 1u)) == 0) {
     sha_finish(a, jb, st);
     if (t == 0) {
       a.ctr->diag[1] = __builtin_amdgcn_s_memtime();
