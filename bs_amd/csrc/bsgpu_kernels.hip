@@ -915,12 +915,13 @@ __device__ __forceinline__ uint32_t block_scan4(uint32_t (&v)[4], uint32_t (&pre
   return total;
 }
 
-// Splits the jobs between the two SHA-256 paths and lays out both queues, longest first.
-// Bucket b (LPT, b = 0 longest) of wave-eligible jobs goes to wave mode iff its longest
-// length is >= tlen and the wave-mode tickets stay <= half the waves. tlen balances the paths:
-// a per-lane job takes ~2.3x the time per block of a wave-mode one (6,820 vs 2,941 cycles), so
-// jobs longer than ~0.43 of the longest would outlast the longest wave-mode job; and no job
-// longer than the per-lane work share (total / lanes) is worth keeping per-lane either.
+// Splits the jobs between the SHA-256 paths and lays out both queues, longest first.
+// Bucket b (LPT, b = 0 longest) of wave-eligible jobs goes to solo / group tickets iff its
+// longest length is >= tlen (BSG_TLEN_PCT of the longest, and the per-lane work share) and
+// those tickets stay <= half the waves; the next buckets down to tlen2 (BSG_PAIR_PCT) go to
+// pair tickets within the rest of that budget. A per-lane job takes ~2.5x the time per block
+// of a skewed-pair one under load (~7,650 vs ~3,030 cycles; ~4,250 with a pair ticket's ring
+// fills), so the longest per-lane job, not the longest chain, would otherwise end the launch.
 __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t nok;
