@@ -1,0 +1,60 @@
+"""Long randomized parity run (not part of pytest): many seeded draws of batch and streaming
+splits against the oracle. python tools/stress_parity.py [N] -- prints a line per 20 draws."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bs_amd import bsgpu  # noqa: E402
+from bs_amd.synth import splitmix_array, splitmix_bytes  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def tuples(ch):
+    return [(int(c["offset"]), int(c["len"]), int(c["level"]), bytes(c["ref"])) for c in ch]
+
+
+def main():
+    n_draws = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    table = O.buzhash32_table(1)
+    t0 = time.time()
+    for d in range(n_draws):
+        rng = np.random.default_rng(70_000 + d)
+        bits = int(rng.integers(10, 23))
+        mn = int(rng.choice([64, 512, 1024, 4096]))
+        if d % 2 == 0:  # batch of streams, lengths up to 8 MB
+            ns = int(rng.integers(1, 40))
+            lens = [int(x) for x in rng.integers(0, 8_000_000, size=ns)]
+            arrs = [splitmix_array(1_000_000 + 97 * d + i, n) for i, n in enumerate(lens)]
+            ch, counts = bsgpu.split_hash_batch(arrs, bits=bits, min_size=mn)
+            k = 0
+            for i, a in enumerate(arrs):
+                want = tuples(O.split(table, a, bits=bits, min_size=mn))
+                got = tuples(ch[k:k + int(counts[i])])
+                assert got == want, ("batch", d, i, bits, mn, len(a))
+                k += int(counts[i])
+        else:  # one stream through the streaming Writer
+            n = int(rng.integers(0, 24_000_000))
+            data = splitmix_bytes(2_000_000 + d, n)
+            tile = int(rng.choice([65536, 1 << 20, 16 << 20]))
+            w = bsgpu.StreamingSplitter(bits=bits, min_size=mn, tile=tile)
+            pos, got = 0, []
+            while pos < n:
+                k = int(rng.choice([4096, 100_000, 4 << 20]))
+                w.write(data[pos:pos + k])
+                pos += k
+                got.append(w.drain())
+            w.close()
+            got.append(w.drain())
+            w.free()
+            want = tuples(O.split(table, np.frombuffer(data, dtype=np.uint8), bits=bits, min_size=mn))
+            assert tuples(np.concatenate(got)) == want, ("stream", d, bits, mn, n, tile)
+        if d % 20 == 19:
+            print(f"{d + 1} draws ok ({time.time() - t0:.0f} s)", flush=True)
+    print(f"all {n_draws} draws bit-identical to the oracle", flush=True)
+
+
+if __name__ == "__main__":
+    main()
