@@ -37,6 +37,20 @@ def test_default_table_matches_golden():
     assert bsgpu.default_table().tolist() == golden.tolist()
 
 
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: with libbsgpu.so absent, every entry of the binding raises."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("from bs_amd import bsgpu\n"
+            "try:\n    bsgpu.split_hash_batch([b'x' * 5000])\n"
+            "except RuntimeError as e:\n    print('RAISED', e)\n")
+    env = dict(os.environ, BSG_LIB_PATH=str(tmp_path / "absent.so"))
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                         text=True, timeout=120)
+    assert "RAISED" in out.stdout and "no CPU fallback" in out.stdout, out.stdout + out.stderr
+
+
 def test_errstr_and_bad_device():
     from bs_amd import bsgpu
     L = bsgpu.lib()
