@@ -18,10 +18,11 @@ def tuples(ch):
 
 def main():
     n_draws = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    seed_base = int(sys.argv[2]) if len(sys.argv) > 2 else 70_000  # new draws: another base
     table = O.buzhash32_table(1)
     t0 = time.time()
     for d in range(n_draws):
-        rng = np.random.default_rng(70_000 + d)
+        rng = np.random.default_rng(seed_base + d)
         bits = int(rng.integers(10, 23))
         mn = int(rng.choice([64, 512, 1024, 4096]))
         if d % 2 == 0:  # batch of streams, lengths up to 8 MB
