@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--bits", type=int, default=16)
     ap.add_argument("--min-size", type=int, default=1024)
     ap.add_argument("--cpu-sample-mib", type=int, default=1024,
-                    help="bytes of stream 0 the CPU oracle baseline splits+hashes (0: skip)")
+                    help="bytes the CPU oracle baseline splits+hashes: a prefix of stream 0 for "
+                         "one stream, else whole streams (at least one per thread) (0: skip)")
     ap.add_argument("--e2e-mib", type=int, default=1024,
                     help="bytes of host-memory stream for the PCIe-inclusive streaming rate "
                          "(bsg_write -> records in host memory; 0: skip)")
@@ -64,6 +65,27 @@ def dist_setup():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend="gloo")
     return world, rank, local
+
+
+def check_world(gpus: int, world: int) -> None:
+    """--gpus N must match the launch: N ranks under torch.distributed.run, one per GPU.
+    A plain `python bench.py --gpus 8` would otherwise time one GPU and report it as n_gpus 1."""
+    if gpus != world:
+        raise SystemExit(
+            f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; launch one rank per GPU: "
+            f"python -m torch.distributed.run --nnodes=1 --nproc-per-node {gpus} "
+            f"--master-addr 127.0.0.1 --master-port P bench.py --gpus {gpus} ...")
+
+
+def build_once(world: int, local: int) -> str:
+    """Local rank 0 builds libbsgpu.so if it is stale (normally a no-op: the tree ships the
+    built library), the other ranks wait at a barrier and then only load it. The build itself
+    is also flock-serialised (bs_amd/build.py), so even concurrent builders compile once."""
+    from bs_amd import build
+    if local == 0:
+        build.build()
+    barrier(world)
+    return build.build()  # fresh after the barrier: returns the path without compiling
 
 
 def barrier(world):
@@ -98,23 +120,44 @@ def timed_steps(step, sync, world: int, steps: int, warmup: int) -> float:
     return max_over_ranks(t1 - t0, world)
 
 
-def cpu_baseline(sample_mib: int, bits: int, min_size: int) -> dict | None:
-    """The C oracle ("port" of the reference's per-stream Splitter + sha256) on this host,
-    one thread (the reference runs one goroutine per stream), over the first sample_mib MiB of
-    stream 0."""
-    if sample_mib <= 0:
+def cpu_threads() -> int:
+    """Host threads for the multi-stream CPU baseline: the GPU box's CPU share (16 per GPU,
+    OMP_NUM_THREADS), not os.cpu_count(), which shows the whole machine there."""
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+
+
+def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str) -> dict | None:
+    """The C oracle ("port" of the reference's per-stream Splitter + sha256: literal per-byte
+    buzhash32 loop, SHA-256 with the x86 SHA extensions when the host has them, as Go's amd64
+    crypto/sha256 does) over a bounded sample of the same bytes on this host. One stream per
+    thread, as the reference runs one goroutine per stream: 1 thread for a single stream,
+    cpu_threads() for a batch."""
+    if not host_streams:
         return None
-    from bs_amd.synth import splitmix_array
+    import numpy as np
     from oracle import oracle as O  # checker / baseline only
-    n = sample_mib << 20
-    data = splitmix_array(BASE_SEED, n)
     table = O.buzhash32_table(1)
-    t0 = time.perf_counter()
-    ch = O.split(table, data, bits=bits, min_size=min_size)
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample_mib} MiB of stream 0 (same bytes/params), C oracle "
-                      f"split+sha256, 1 thread, {len(ch)} chunks in {dt:.2f}s"}
+    impl = O.sha256_use(True)
+    n = sum(len(a) for a in host_streams)
+    if len(host_streams) == 1:
+        threads = 1
+        t0 = time.perf_counter()
+        ch = O.split(table, host_streams[0], bits=bits, min_size=min_size)
+        dt = time.perf_counter() - t0
+        nch = len(ch)
+    else:
+        threads = min(cpu_threads(), len(host_streams))
+        base = np.concatenate(host_streams)
+        lens = [len(a) for a in host_streams]
+        off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        t0 = time.perf_counter()
+        ch, _ = O.split_streams(table, base, off, lens, bits=bits, min_size=min_size,
+                                threads=threads)
+        dt = time.perf_counter() - t0
+        nch = len(ch)
+    return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{sample} (same bytes/params), C oracle split + sha256 ({impl}), "
+                      f"{threads} thread(s), one stream per thread, {nch} chunks in {dt:.2f}s"}
 
 
 def chain_roofline(diag: dict) -> dict | None:
@@ -191,9 +234,10 @@ def pmc_traffic(kernel: str, workload: str):
 def main():
     args = parse()
     world, rank, local = dist_setup()
-    from bs_amd import build, bsgpu
+    check_world(args.gpus, world)
+    from bs_amd import bsgpu
 
-    build.build()
+    build_once(world, local)
     assert bsgpu.device_count() > local, "bench.py needs a GPU (the HIP path is the product)"
     nbytes = args.stream_mib << 20
     ns = args.streams
@@ -244,12 +288,23 @@ def main():
         check = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
                      and (got["offset"] == ref["offset"]).all())
     diag = eng.diag()
-    # the device-resident engine and its 1 GiB input are done with: free them, so the streaming
+    # the CPU baseline's sample: the same device bytes, copied back after timing
+    host_streams, sample = [], ""
+    if rank == 0 and world == 1 and args.cpu_sample_mib > 0:
+        want = args.cpu_sample_mib << 20
+        if ns == 1:
+            host_streams = [buf.to_host(0, min(nbytes, want))]
+            sample = f"first {len(host_streams[0]) >> 20} MiB of stream 0"
+        else:
+            k = min(ns, max(4 * cpu_threads(), -(-want // nbytes)))
+            host_streams = [buf.to_host(offs[i], nbytes) for i in range(k)]
+            sample = f"streams 0..{k - 1} of {ns} ({k} x {args.stream_mib} MiB)"
+    # the device-resident engine and its input are done with: free them, so the streaming
     # measurement below has the GPU's hardware queues and memory to itself
     eng.close()
     buf.free()
-    cpu = cpu_baseline(args.cpu_sample_mib, args.bits, args.min_size) \
-        if (rank == 0 and world == 1) else None
+    cpu = cpu_baseline(host_streams, args.bits, args.min_size, sample)
+    del host_streams
     e2e = end_to_end(args.e2e_mib, args.bits, args.min_size, local) \
         if (rank == 0 and world == 1) else None
     workload = ("configs[1]: 1 GiB random stream per GPU, default split params"

@@ -21,7 +21,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "bsgpu.h")
 
 BSG_OK = 0
 READ_SLACK = 256  # BSG_READ_SLACK: readable bytes required after the last stream
-ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EDEVICE", -71: "ESTATE", -19: "ENODEV"}
+ERRORS = {-22: "EINVAL", -12: "ENOMEM", -5: "EDEVICE", -71: "ESTATE", -19: "ENODEV",
+          -2: "ENOTFOUND", -74: "ECORRUPT", -1001: "EIO"}
 
 
 class BsgError(RuntimeError):
@@ -114,6 +115,9 @@ def lib() -> ctypes.CDLL:
         "bsg_store_put_ref": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_int)]),
         "bsg_store_list_from": (ctypes.c_size_t, [vp, vp, vp, ctypes.c_size_t]),
+        "bsg_store_delete": (ctypes.c_int, [vp, vp]),
+        "bsg_split_protect": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_size_t)]),
         "bsg_writer_new": (vp, [ctypes.c_int, vp, ctypes.POINTER(Params), ctypes.c_size_t,
                                 ctypes.POINTER(ctypes.c_int)]),
         "bsg_writer_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
@@ -188,7 +192,7 @@ def split_hash_batch(streams: list[bytes] | list[np.ndarray], bits: int = 16,
     base = np.concatenate(arrs) if arrs else np.zeros(1, np.uint8)
     if base.size == 0:
         base = np.zeros(1, np.uint8)
-    cap = int(sum(int(l) // min_size + 2 for l in lens)) + 1
+    cap = int(sum(int(l) // (min_size or 64) + 2 for l in lens)) + 1
     out = np.zeros(cap, dtype=CHUNK_DTYPE)
     counts = np.zeros(max(len(arrs), 1), dtype=np.uint64)
     n = ctypes.c_uint64(0)
@@ -438,7 +442,6 @@ class StreamingSplitter:
 NOT_FOUND = -2    # BSG_ENOTFOUND = bs.ErrNotFound
 CORRUPT = -74     # BSG_ECORRUPT: a fetched chunk does not hash to its ref (Reader verify)
 READER_VERIFY = 1
-ERRORS.update({NOT_FOUND: "ENOTFOUND", CORRUPT: "ECORRUPT", -1001: "EIO"})
 
 
 class MemStore:
@@ -489,6 +492,22 @@ class MemStore:
 
     def __len__(self) -> int:
         return lib().bsg_store_count(self.h)
+
+    def delete(self, ref: bytes) -> None:
+        """bs.DeleterStore.Delete (store/mem only)."""
+        _check(lib().bsg_store_delete(self.h, bytes(ref)), "Delete")
+
+    def protect_children(self, ref: bytes) -> list[tuple[bytes, bool]]:
+        """split.Protect (split/split.go:306-322): [(child ref, traverse?)] of the Node at ref,
+        child nodes (traverse=True) first, then leaves."""
+        n = ctypes.c_size_t(0)
+        _check(lib().bsg_split_protect(self.h, bytes(ref), None, None, 0, ctypes.byref(n)),
+               "Protect")
+        refs = ctypes.create_string_buffer(32 * max(n.value, 1))
+        trav = ctypes.create_string_buffer(max(n.value, 1))
+        _check(lib().bsg_split_protect(self.h, bytes(ref), refs, trav, n.value, ctypes.byref(n)),
+               "Protect")
+        return [(refs.raw[32 * i:32 * i + 32], trav.raw[i] == 1) for i in range(n.value)]
 
     def free(self):
         if self.h:

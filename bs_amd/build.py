@@ -35,17 +35,53 @@ def build_debug(extra=(), name="libbsgpu_dbg.so") -> str:
     return out
 
 
+def build_locked(out: str, stale, compile_to) -> bool:
+    """Runs compile_to(tmp) and renames tmp to `out` if stale() holds, under an exclusive
+    flock on out + ".lock", so concurrent builders (bench ranks, test workers) compile once:
+    the others wait, re-check stale() and find the fresh library. The temporary file is per
+    process and the rename is atomic, so a process loading `out` never sees a partial file.
+    Returns True if this call compiled."""
+    import fcntl
+    with open(out + ".lock", "a") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not stale():
+                return False
+            tmp = f"{out}.tmp.{os.getpid()}"
+            try:
+                compile_to(tmp)
+                os.replace(tmp, out)
+            finally:
+                if os.path.exists(tmp):
+                    os.unlink(tmp)
+            return True
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result", "-o", LIB + ".tmp"]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+
+    def compile_to(tmp):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result",
+               "-o", tmp]
+        cmd += [os.path.join(CSRC, f) for f in SOURCES]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+
+    forced = [force]
+
+    def stale():
+        if forced[0]:
+            forced[0] = False
+            return True
+        return _stale()
+
+    build_locked(LIB, stale, compile_to)
     return LIB
 
 

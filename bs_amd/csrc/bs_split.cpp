@@ -88,6 +88,12 @@ Status MemStore::ListRefs(const Ref& start, const std::function<Status(const Ref
   return Status::Ok();
 }
 
+Status MemStore::Delete(const Ref& ref) {  // mem.go:79-85
+  std::lock_guard<std::mutex> g(mu_);
+  blobs_.erase(ref);
+  return Status::Ok();
+}
+
 size_t MemStore::Size() const {
   std::lock_guard<std::mutex> g(mu_);
   return blobs_.size();
@@ -496,6 +502,16 @@ Status get_node(Store* g, const Ref& ref, Node* n) {
 }
 }  // namespace
 
+Status Protect(Store* g, const Ref& ref, std::vector<ProtectPair>* out) {  // split.go:306-322
+  out->clear();
+  Node n;
+  Status s = get_node(g, ref, &n);
+  if (!s.ok()) return s;
+  for (const Child& c : n.nodes) out->push_back(ProtectPair{c.ref, true});
+  for (const Child& c : n.leaves) out->push_back(ProtectPair{c.ref, false});
+  return Status::Ok();
+}
+
 std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err, bool verify,
                                     int device) {
   Status dummy;
@@ -559,11 +575,15 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
     for (;;) {  // descend to the leaf node
       const Node& node = stack_.back();
       if (!node.leaves.empty()) break;
+      if (node.nodes.empty()) return Status::Err(kCorrupt, "tree node with no children");
       size_t index = 0;
       if (pos_ > node.offset) {
         index = std::upper_bound(node.nodes.begin(), node.nodes.end(), pos_,
                                  [](uint64_t p, const Child& c) { return c.offset > p; }) -
                 node.nodes.begin();
+        // sort.Search (split.go:222-225) would index out of range here; a Go panic, a
+        // corrupt-tree error for us
+        if (index == 0) return Status::Err(kCorrupt, "tree node offsets past the read position");
         index--;
       }
       Node child;
@@ -586,8 +606,13 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
         if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
       }
       const std::vector<uint8_t>& chunk = verify_ ? cache_[k] : fetched;
+      // offsets come from store contents: check them before indexing (Go's bounds checks
+      // would panic on the same trees)
+      if (leaves[k].offset > pos_ || pos_ - leaves[k].offset > chunk.size())
+        return Status::Err(kCorrupt, "leaf offsets do not match chunk sizes");
       const uint64_t skip = pos_ - leaves[k].offset;
       const size_t avail = chunk.size() - (size_t)skip;
+      if (avail == 0) return Status::Err(kCorrupt, "leaf offsets do not match chunk sizes");
       const size_t take = std::min(avail, len);
       std::memcpy(buf, chunk.data() + skip, take);
       buf += take;
@@ -695,6 +720,30 @@ int bsg_store_put_ref(bsg_store* s, const uint8_t ref[32], const uint8_t* data, 
   bs::Status st = rp->PutWithRef(r, n ? data : &empty, n, &a);
   if (!st.ok()) return st.code;
   if (added) *added = a ? 1 : 0;
+  return BSG_OK;
+}
+
+int bsg_store_delete(bsg_store* s, const uint8_t ref[32]) {
+  if (!s || !ref) return BSG_EINVAL;
+  if (!s->mem) return BSG_EINVAL;  // store/file is not a bs.DeleterStore
+  bs::Ref r;
+  std::memcpy(r.data(), ref, 32);
+  return s->mem->Delete(r).code;
+}
+
+int bsg_split_protect(bsg_store* s, const uint8_t ref[32], uint8_t* refs, uint8_t* traverse,
+                      size_t cap, size_t* n) {
+  if (!s || !ref || !n) return BSG_EINVAL;
+  bs::Ref r;
+  std::memcpy(r.data(), ref, 32);
+  std::vector<bs::split::ProtectPair> pairs;
+  bs::Status st = bs::split::Protect(s->st.get(), r, &pairs);
+  if (!st.ok()) return st.code;
+  *n = pairs.size();
+  for (size_t i = 0; i < pairs.size() && i < cap; ++i) {
+    if (refs) std::memcpy(refs + 32 * i, pairs[i].ref.data(), 32);
+    if (traverse) traverse[i] = pairs[i].traverse ? 1 : 0;
+  }
   return BSG_OK;
 }
 

@@ -141,10 +141,15 @@ int long_mode() {  // BSG_LONG_MODE = off | all (experiments); default auto
 
 int normalize(const bsg_params* in, Params* out, bsg_params* norm) {
   bsg_params p = in ? *in : bsg_params_default();
+  // Every value split.Bits / split.MinSize accept (split/split.go:137-152 store them unchecked)
+  // is valid: 0 takes hashsplit's default (SplitBits 13, MinSize 64 = the window); MinSize 1..63
+  // lets a window span a boundary (the hash still depends only on the last 64 stream bytes, so
+  // nothing changes but the greedy rule); Bits > 32 can never be met by TrailingZeros32 (<= 32),
+  // so the stream is one final chunk. fanout 0 is our C default (Fanout(0) in Go would divide by
+  // zero in split.go:86).
   if (p.split_bits == 0) p.split_bits = 13;  // hashsplit defaultSplitBits
   if (p.min_size == 0) p.min_size = 64;      // hashsplit defaultMinSize (window size)
   if (p.fanout == 0) p.fanout = 8;
-  if (p.split_bits > 32 || p.min_size < 64) return BSG_EINVAL;
   out->split_bits = p.split_bits;
   out->min_size = p.min_size;
   out->mask = p.split_bits >= 32 ? 0xffffffffu : ((1u << p.split_bits) - 1u);
@@ -201,7 +206,6 @@ struct bsg_engine {
     }
     s0[ns] = strips;
     nstrips = strips;
-    chunk_cap = chunk_bound;
     {
       // random input yields ~len/2^bits candidates; degenerate input (e.g. all zeros: one per
       // byte) overflows this estimate and is re-run once at its exact size by finish().
@@ -209,6 +213,10 @@ struct bsg_engine {
       cand_cap = std::max<uint64_t>(1u << 16, ((total_len >> b) << 2) + 2ull * ns + 1024);
       if (retry_cap > cand_cap) cand_cap = retry_cap;
     }
+    // Every chunk ends at a candidate (the forced final one included), and a run whose
+    // candidates overflow cand_cap selects nothing, so cand_cap also bounds the chunk count; it
+    // is the tighter bound for small MinSize (len / MinSize records would be ~len for MinSize 1).
+    chunk_cap = std::min(chunk_bound, cand_cap);
     HCHECK(streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(strip0.ensure(sizeof(uint64_t) * (ns + 1)));
     HCHECK(counts.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
@@ -775,6 +783,9 @@ const char* bsg_errstr(int err) {
     case BSG_EDEVICE: return "HIP device error";
     case BSG_ESTATE: return "invalid state (write after close?)";
     case BSG_ENODEV: return "no such HIP device";
+    case BSG_ENOTFOUND: return "not found";
+    case BSG_ECORRUPT: return "blob does not match its ref";
+    case BSG_EIO: return "filesystem error";
     default: return "unknown error";
   }
 }

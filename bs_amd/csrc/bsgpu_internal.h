@@ -78,9 +78,9 @@ struct ChunkRec {              // == bsg_chunk (include/bsgpu.h)
 static_assert(sizeof(ChunkRec) == 56, "ChunkRec layout");
 
 struct Params {
-  uint32_t split_bits;         // trailing-zero bits for a boundary (1..32)
-  uint32_t min_size;           // minimum chunk size (>= 64)
-  uint32_t mask;               // (1 << split_bits) - 1
+  uint32_t split_bits;         // trailing-zero bits for a boundary (>= 1; > 32 never splits)
+  uint32_t min_size;           // minimum chunk size (>= 1)
+  uint32_t mask;               // (1 << split_bits) - 1, all ones for split_bits >= 32
   uint32_t pad_;
 };
 

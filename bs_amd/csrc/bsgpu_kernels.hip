@@ -136,7 +136,7 @@ __device__ __noinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, 
   load16(d + off, w);
   if (off >= 64) load16(d + off - 64, pw);
   else load16(sd->hist, pw);
-  const uint32_t mask = a.p.mask;
+  const uint32_t bits = a.p.split_bits;
   uint32_t h = 0;
 #pragma unroll
   for (int k = 0; k < 64; ++k) h = rotl1(h) ^ lookup(tab, pw[k >> 2], lane4, k);
@@ -145,7 +145,10 @@ __device__ __noinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, 
     uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
     uint32_t tout = lookup(tab, pw[k >> 2], lane4, k);
     h = xor3(rotl1(h), tout, tin);
-    if ((h & mask) == 0) emit<WRITE>(a, c, strip, off + k, false, tz32(h));
+    // the exact test (the pre-filter's mask test is equivalent for bits <= 32; Bits > 32 never
+    // splits, hashsplit's tz >= SplitBits with tz <= 32)
+    const uint32_t tz = tz32(h);
+    if (tz >= bits) emit<WRITE>(a, c, strip, off + k, false, tz);
   }
 }
 
@@ -315,7 +318,6 @@ __device__ __forceinline__ uint32_t scan_strip(const ScanArgs& a, const uint32_t
   c.seg_base = sd->seg_base;
   const uint32_t len = (uint32_t)min((uint64_t)kStrip, seglen - c.start);
   const uint8_t* d = a.data + sd->data_off;
-  const uint32_t mask = a.p.mask;
 
   uint32_t w[16];
   if (c.start >= 64) load16(d + c.start - 64, w);
@@ -345,7 +347,8 @@ __device__ __forceinline__ uint32_t scan_strip(const ScanArgs& a, const uint32_t
         uint32_t t = lds_at(tab, (byte << 8) | lane4);
         h = xor3(rotl1(h), hist[k], t);
         hist[k] = t;
-        if ((h & mask) == 0) emit<WRITE>(a, c, strip, off + k, false, tz32(h));
+        const uint32_t tz = tz32(h);
+        if (tz >= a.p.split_bits) emit<WRITE>(a, c, strip, off + k, false, tz);
       }
     }
   }

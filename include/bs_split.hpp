@@ -88,6 +88,9 @@ class MemStore : public Store, public RefPutter {
   Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) override;
   Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
   Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
+  // bs.DeleterStore (store.go:50-54): removes ref if present; absent refs are not an error
+  // (mem.go:79-85).
+  Status Delete(const Ref& ref);
   size_t Size() const;
 
  private:
@@ -183,6 +186,15 @@ class Writer {
   bool closed_ = false;
   Status sticky_;
 };
+
+// split.Protect (split/split.go:306-322), the gc.ProtectFunc for split trees: the children of
+// the Node stored at ref, tree nodes first (each to be traversed the same way), then leaves
+// (chunks, not traversed).
+struct ProtectPair {
+  Ref ref{};
+  bool traverse = false;  // true: a child Node (ProtectPair.F = Protect); false: a leaf
+};
+Status Protect(Store* g, const Ref& ref, std::vector<ProtectPair>* out);
 
 class Reader {
  public:

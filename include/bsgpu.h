@@ -34,7 +34,7 @@ extern "C" {
 #endif
 
 #define BSG_OK 0
-#define BSG_EINVAL (-22)   /* bad argument (e.g. min_size < 64, split_bits > 32) */
+#define BSG_EINVAL (-22)   /* bad argument (null pointer, unaligned stream offset, ...) */
 #define BSG_ENOMEM (-12)   /* host or device allocation failed */
 #define BSG_EDEVICE (-5)   /* HIP runtime / kernel error */
 #define BSG_ESTATE (-71)   /* Write after Close, etc. */
@@ -45,11 +45,15 @@ extern "C" {
 
 /* split.Writer options. Zero fields take hashsplit's own defaults (SplitBits 13, MinSize 64);
  * bsg_params_default() gives split.NewWriter's defaults (16 / 1024 / fanout 8,
- * split/split.go:48,88-89). */
+ * split/split.go:48,88-89). Like split.Bits / split.MinSize (split/split.go:137-152, which
+ * store the value unchecked), every value is accepted: MinSize 1..63 lets the 64-byte window
+ * span a boundary (allowed, only discouraged by split.go:146), and Bits > 32 never splits
+ * (TrailingZeros32 is at most 32), so the whole stream is one final chunk of level 0. A cgo
+ * caller maps MinSize(n <= 0) to 0 (hashsplit's default) and clamps Bits to 2^32-1. */
 typedef struct bsg_params {
-  uint32_t split_bits; /* Bits(n): trailing zero bits for a boundary, 1..32 */
-  uint32_t min_size;   /* MinSize(n): minimum chunk size, >= 64 */
-  uint32_t fanout;     /* Fanout(n): tree level divisor (host tree only), >= 1 */
+  uint32_t split_bits; /* Bits(n): trailing zero bits for a boundary (0 = 13) */
+  uint32_t min_size;   /* MinSize(n): minimum chunk size (0 = 64) */
+  uint32_t fanout;     /* Fanout(n): tree level divisor (host tree only; 0 = 8) */
   uint32_t reserved;
 } bsg_params;
 
@@ -189,6 +193,14 @@ int bsg_store_put_ref(bsg_store* s, const uint8_t ref[32], const uint8_t* data, 
 size_t bsg_store_list_from(bsg_store* s, const uint8_t start[32], uint8_t* refs, size_t cap);
 /* All refs in lexicographic order (32 bytes each, up to cap); returns the total count. */
 size_t bsg_store_list(bsg_store* s, uint8_t* refs, size_t cap);
+/* bs.DeleterStore.Delete (store.go:50-54) for store/mem (mem.go:79-85): absent refs are not an
+ * error. BSG_EINVAL for store/file, which is not a DeleterStore in the reference. */
+int bsg_store_delete(bsg_store* s, const uint8_t ref[32]);
+/* split.Protect (split/split.go:306-322), gc's traversal of a split tree: the children of the
+ * Node stored at ref, child nodes first (traverse[i] = 1: protect them recursively), then its
+ * leaves (traverse[i] = 0). Up to cap refs (32 bytes each); *n = the number of children. */
+int bsg_split_protect(bsg_store* s, const uint8_t ref[32], uint8_t* refs, uint8_t* traverse,
+                      size_t cap, size_t* n);
 
 typedef struct bsg_writer bsg_writer; /* split.NewWriter / Write / Close / Root */
 bsg_writer* bsg_writer_new(int device, bsg_store* s, const bsg_params* params, size_t tile,

@@ -22,7 +22,8 @@
  *                Close emits the non-empty remainder with level from the same check (0 if the
  *                check fails).                                                      [recalled]
  *                BS wiring: split/split.go:85-89 (callback, MinSize 1024, SplitBits 16).
- *   sha256       FIPS 180-4; bs.Blob.Ref (bs.go:24-26) = crypto/sha256.Sum256.
+ *   sha256       FIPS 180-4; bs.Blob.Ref (bs.go:24-26) = crypto/sha256.Sum256. Scalar, or with
+ *                the x86 SHA extensions when the host has them (as Go's amd64 crypto/sha256).
  */
 #include "bsoracle.h"
 
@@ -253,11 +254,90 @@ static void sha256_block(uint32_t st[8], const uint8_t* p) {
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+/* The same compression with the x86 SHA extensions (SHA-NI), when the host has them. Go's
+ * crypto/sha256 (bs.go:25) uses them on amd64 (sha256block_amd64.s), so the CPU baseline uses
+ * them too; both implementations are checked against each other and the FIPS/hashlib vectors.
+ * The state is kept as the instructions want it: ABEF in one register, CDGH in the other.
+ * Group g of four rounds adds K[4g..4g+3] to message words W[4g..4g+3]; W[16..63] come from
+ * sha256msg1 (sigma0 part, issued three groups ahead) and sha256msg2 (sigma1 part). */
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <immintrin.h>
+__attribute__((target("sha,sse4.1,ssse3")))
+static void sha256_blocks_ni(uint32_t st[8], const uint8_t* p, size_t nblocks) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i t = _mm_loadu_si128((const __m128i*)&st[0]);    /* A B C D (low to high) */
+    __m128i s1 = _mm_loadu_si128((const __m128i*)&st[4]);   /* E F G H */
+    t = _mm_shuffle_epi32(t, 0xB1);                          /* B A D C */
+    s1 = _mm_shuffle_epi32(s1, 0x1B);                        /* H G F E */
+    __m128i s0 = _mm_alignr_epi8(t, s1, 8);                  /* F E B A = "ABEF" */
+    s1 = _mm_blend_epi16(s1, t, 0xF0);                       /* H G D C = "CDGH" */
+    for (size_t b = 0; b < nblocks; b++, p += 64) {
+        const __m128i save0 = s0, save1 = s1;
+        __m128i m[4];
+        for (int i = 0; i < 4; i++)
+            m[i] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(p + 16 * i)), bswap);
+        for (int g = 0; g < 16; g++) {
+            __m128i k = _mm_add_epi32(m[g & 3], _mm_loadu_si128((const __m128i*)&K256[4 * g]));
+            s1 = _mm_sha256rnds2_epu32(s1, s0, k);
+            if (g >= 3 && g <= 14) /* W[4g+4..4g+7], before m[(g-1)&3] takes its msg1 below */
+                m[(g + 1) & 3] = _mm_sha256msg2_epu32(
+                    _mm_add_epi32(m[(g + 1) & 3], _mm_alignr_epi8(m[g & 3], m[(g - 1) & 3], 4)),
+                    m[g & 3]);
+            s0 = _mm_sha256rnds2_epu32(s0, s1, _mm_shuffle_epi32(k, 0x0E));
+            if (g >= 1 && g <= 12) m[(g - 1) & 3] = _mm_sha256msg1_epu32(m[(g - 1) & 3], m[g & 3]);
+        }
+        s0 = _mm_add_epi32(s0, save0);
+        s1 = _mm_add_epi32(s1, save1);
+    }
+    t = _mm_shuffle_epi32(s0, 0x1B);                         /* A B E F */
+    s1 = _mm_shuffle_epi32(s1, 0xB1);                        /* C D G H */
+    s0 = _mm_blend_epi16(t, s1, 0xF0);                       /* A B C D */
+    s1 = _mm_alignr_epi8(s1, t, 8);                          /* E F G H */
+    _mm_storeu_si128((__m128i*)&st[0], s0);
+    _mm_storeu_si128((__m128i*)&st[4], s1);
+}
+
+static int host_has_sha_ni(void) {
+    unsigned a, b, c, d;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return 0;
+    if (!(b & (1u << 29))) return 0;                      /* SHA */
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return 0;
+    return (c & (1u << 19)) && (c & (1u << 9));           /* SSE4.1, SSSE3 */
+}
+#else
+static void sha256_blocks_ni(uint32_t st[8], const uint8_t* p, size_t nblocks) {
+    (void)st; (void)p; (void)nblocks;
+}
+static int host_has_sha_ni(void) { return 0; }
+#endif
+
+/* -1: not probed; 0: scalar; 1: SHA-NI. bso_sha256_use(0) forces scalar (tests). */
+static volatile int g_sha_impl = -1;
+
+int bso_sha256_use(int want_ni) {
+    g_sha_impl = (want_ni && host_has_sha_ni()) ? 1 : 0;
+    return g_sha_impl;
+}
+
+int bso_sha256_impl(void) {
+    if (g_sha_impl < 0) g_sha_impl = host_has_sha_ni();
+    return g_sha_impl;
+}
+
+static void sha256_blocks(uint32_t st[8], const uint8_t* p, size_t nblocks) {
+    if (bso_sha256_impl() == 1) {
+        sha256_blocks_ni(st, p, nblocks);
+        return;
+    }
+    for (size_t i = 0; i < nblocks; i++) sha256_block(st, p + 64 * i);
+}
+
 void bso_sha256(const uint8_t* data, size_t n, uint8_t out[32]) {
     uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                       0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
     size_t full = n / 64;
-    for (size_t i = 0; i < full; i++) sha256_block(st, data + 64 * i);
+    sha256_blocks(st, data, full);
     uint8_t tail[128];
     size_t r = n - 64 * full;
     memset(tail, 0, sizeof tail);
@@ -266,8 +346,7 @@ void bso_sha256(const uint8_t* data, size_t n, uint8_t out[32]) {
     size_t tl = (r + 9 <= 64) ? 64 : 128;
     uint64_t bits = (uint64_t)n * 8;
     for (int i = 0; i < 8; i++) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
-    sha256_block(st, tail);
-    if (tl == 128) sha256_block(st, tail + 64);
+    sha256_blocks(st, tail, tl / 64);
     for (int i = 0; i < 8; i++) {
         out[4 * i] = (uint8_t)(st[i] >> 24);
         out[4 * i + 1] = (uint8_t)(st[i] >> 16);
@@ -301,17 +380,26 @@ static size_t split_one(const uint32_t table[256], const uint8_t* x, size_t n, u
     if (split_bits == 0) split_bits = 13; /* hashsplit defaultSplitBits */
     size_t k = 0;
     uint64_t start = 0;
+    /* Buzhash32.Roll with the state in locals: the window is read back from the stream (the
+     * byte leaving a 64-byte window is x[p-64], or a priming zero before the stream), which is
+     * what the ring buffer holds; the sum stays in a register (a uint8_t ring store would alias
+     * it and force a reload per byte). */
+    uint32_t sum = d.sum;
+    const uint32_t T0 = table[0];
     for (size_t p = 0; p < n; p++) {
-        buzhash32_roll(&d, x[p]);              /* s.chunk = append(s.chunk, c); s.rs.Roll(c) */
+        const uint32_t h0 = p >= 64 ? table[x[p - 64]] : T0;
+        sum = rotl32(sum, 1) ^ h0 ^ table[x[p]];  /* rotl(h0, 64 % 32) = h0 */
+        /* s.chunk = append(s.chunk, c); s.rs.Roll(c) */
         uint64_t len = (uint64_t)p + 1 - start;
         if (len < min_size) continue;          /* if len(s.chunk) < minSize { continue } */
-        unsigned tz = tz32(d.sum);             /* checkSplit */
+        unsigned tz = tz32(sum);               /* checkSplit */
         if (tz >= split_bits) {
             emit(out, cap, k, x, start, len, tz - split_bits, with_refs, stream);
             k++;
             start = (uint64_t)p + 1;           /* s.chunk = nil; Reset=false: no re-prime */
         }
     }
+    d.sum = sum;
     if (start < n) {                           /* Close(): flush the remainder */
         unsigned tz = tz32(d.sum);
         unsigned level = (tz >= split_bits) ? tz - split_bits : 0;
@@ -350,9 +438,11 @@ static void* mt_worker(void* arg) {
         if (s >= j->nstreams) break;
         const uint8_t* x = j->base + j->off[s];
         size_t n = (size_t)j->len[s];
-        size_t c = split_one(j->table, x, n, j->bits, j->min_size, 0, NULL, 0, s);
-        bso_chunk* buf = (bso_chunk*)malloc((c ? c : 1) * sizeof(bso_chunk));
-        split_one(j->table, x, n, j->bits, j->min_size, 1, buf, c, s);
+        /* one pass: every non-final chunk has >= MinSize bytes */
+        const size_t ms = j->min_size ? j->min_size : 64;
+        const size_t bound = n / ms + 1;
+        bso_chunk* buf = (bso_chunk*)malloc(bound * sizeof(bso_chunk));
+        size_t c = split_one(j->table, x, n, j->bits, j->min_size, 1, buf, bound, s);
         j->tmp[s] = buf;
         j->cnt[s] = c;
     }

@@ -45,6 +45,11 @@ void bso_rolling_sums(const uint32_t table[256], const uint8_t* x, size_t n, uin
 
 /* ---- SHA-256 (FIPS 180-4) ---- */
 void bso_sha256(const uint8_t* data, size_t n, uint8_t out[32]);
+/* Which compression bso_sha256 uses: 1 = x86 SHA extensions (detected by cpuid, the default
+ * when present, as Go's crypto/sha256 does on amd64), 0 = portable scalar C. */
+int bso_sha256_impl(void);
+/* Select it (want_ni = 0 forces scalar); returns the implementation now in use. */
+int bso_sha256_use(int want_ni);
 
 /* ---- hashsplit Splitter restatement (per byte, literal) ----
  * Returns the number of chunks; writes at most `cap` chunk records (offset/len/level, and the

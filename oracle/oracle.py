@@ -62,6 +62,9 @@ def lib():
         L.bso_buzhash32_generate.argtypes = [ctypes.c_int64, u32p]
         L.bso_rolling_sums.argtypes = [u32p, u8p, ctypes.c_size_t, u32p]
         L.bso_sha256.argtypes = [u8p, ctypes.c_size_t, u8p]
+        L.bso_sha256_impl.restype = ctypes.c_int
+        L.bso_sha256_use.restype = ctypes.c_int
+        L.bso_sha256_use.argtypes = [ctypes.c_int]
         L.bso_split.restype = ctypes.c_size_t
         L.bso_split.argtypes = [u32p, u8p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint,
                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
@@ -106,6 +109,16 @@ def sha256(data: bytes | np.ndarray) -> bytes:
     return out.tobytes()
 
 
+def sha256_impl() -> str:
+    """'sha-ni' or 'scalar': the compression the C oracle's SHA-256 uses on this host."""
+    return "sha-ni" if lib().bso_sha256_impl() == 1 else "scalar"
+
+
+def sha256_use(ni: bool) -> str:
+    """Select SHA-NI (when the host has it) or the scalar compression; returns the one in use."""
+    return "sha-ni" if lib().bso_sha256_use(int(ni)) == 1 else "scalar"
+
+
 def split(table: np.ndarray, data, bits: int = 16, min_size: int = 1024,
           with_refs: bool = True) -> np.ndarray:
     """Chunks of one stream as a CHUNK_DTYPE array (offset, len, level, stream=0, ref)."""
@@ -113,12 +126,14 @@ def split(table: np.ndarray, data, bits: int = 16, min_size: int = 1024,
     x = np.ascontiguousarray(x, dtype=np.uint8)
     t = np.ascontiguousarray(table, dtype=np.uint32)
     L = lib()
-    n = L.bso_split(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits, min_size, 0,
-                    None, 0)
-    out = np.zeros(max(n, 1), dtype=CHUNK_DTYPE)
-    L.bso_split(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits, min_size,
-                int(with_refs), out.ctypes.data, n)
-    return out[:n]
+    # one pass: every non-final chunk has >= MinSize bytes, so len // MinSize + 1 records fit
+    ms = min_size if min_size > 0 else 64
+    cap = len(x) // ms + 1
+    out = np.empty(max(cap, 1), dtype=CHUNK_DTYPE)
+    n = L.bso_split(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits, min_size,
+                    int(with_refs), out.ctypes.data, cap)
+    assert n <= cap
+    return out[:n].copy() if n < cap // 2 else out[:n]
 
 
 def split_streams(table: np.ndarray, base: np.ndarray, off, lens, bits: int = 16,
@@ -129,7 +144,8 @@ def split_streams(table: np.ndarray, base: np.ndarray, off, lens, bits: int = 16
     lens = np.ascontiguousarray(lens, dtype=np.uint64)
     base = np.ascontiguousarray(base, dtype=np.uint8)
     counts = np.zeros(len(off), dtype=np.uint64)
-    cap = int(sum(int(l) // max(min_size, 64) + 1 for l in lens))
+    ms = min_size if min_size > 0 else 64  # hashsplit: MinSize 0 means the 64-byte window
+    cap = int(sum(int(l) // ms + 1 for l in lens))
     out = np.zeros(max(cap, 1), dtype=CHUNK_DTYPE)
     n = lib().bso_split_streams(_p(t, ctypes.c_uint32), _p(base, ctypes.c_uint8),
                                 _p(off, ctypes.c_uint64), _p(lens, ctypes.c_uint64), len(off),
@@ -183,6 +199,9 @@ class PyChunk:
 
 
 def py_split(table, data: bytes, bits: int = 16, min_size: int = 1024) -> list[PyChunk]:
+    # hashsplit's zero defaults: SplitBits 0 -> 13, MinSize <= 0 -> 64 (the window) [recalled]
+    bits = bits or 13
+    min_size = min_size if min_size > 0 else 64
     sums = py_rolling_sums(table, data)
     out, start = [], 0
     for p, h in enumerate(sums):

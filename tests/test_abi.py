@@ -60,6 +60,16 @@ def test_errstr_and_bad_device():
     n = L.bsg_device_count()
     h = L.bsg_open(n + 3, None, None, ctypes.byref(err))  # no such device
     assert not h and err.value == -19
-    bad = bsgpu.Params(16, 32, 8, 0)  # MinSize below the 64-byte window
-    h = L.bsg_open(0, ctypes.byref(bad), None, ctypes.byref(err))
-    assert not h and err.value == -22
+    for code, text in ((-2, b"not found"), (-74, b"blob does not match its ref"),
+                       (-1001, b"filesystem error"), (-12, b"out of memory")):
+        assert L.bsg_errstr(code) == text
+    # MinSize below the window and Bits above 32 are valid (split.go:137-152 accept any value):
+    # never EINVAL; without a GPU the open fails only for want of a device
+    for bits, mn in ((16, 32), (16, 1), (33, 64), (2**32 - 1, 1)):
+        p = bsgpu.Params(bits, mn, 8, 0)
+        h = L.bsg_open(0, ctypes.byref(p), None, ctypes.byref(err))
+        if n == 0:
+            assert not h and err.value == -19
+        else:
+            assert h and err.value == 0
+            L.bsg_free(h)

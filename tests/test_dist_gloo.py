@@ -32,6 +32,14 @@ def _worker(rank, world, port, q):
     from oracle import oracle as O
     w, r, local = bench.dist_setup()
     assert (w, r) == (world, rank)
+    bench.check_world(world, w)                 # --gpus N == WORLD_SIZE passes
+    try:
+        bench.check_world(world + 1, w)         # a mismatch must stop the bench
+        raise AssertionError("check_world accepted a wrong --gpus")
+    except SystemExit:
+        pass
+    lib = bench.build_once(w, local)            # rank 0 builds (if stale), the others wait
+    assert os.path.exists(lib)
     table = O.buzhash32_table(1)
     data = splitmix_array(bench.BASE_SEED + r, 1 << 20)  # rank r's own stream
     out = {}
@@ -63,3 +71,49 @@ def test_two_rank_harness():
     assert e0 >= 0.1                        # >= rank 1's two sleeps
     assert b0 == b1 == 1 << 20              # each rank split its whole stream
     assert c0 > 0 and c1 > 0
+
+
+def _racer(out, q):
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from bs_amd import build
+
+    def compile_to(tmp):
+        time.sleep(0.3)  # a slow compiler: the racers overlap
+        with open(tmp, "w") as f:
+            f.write(f"built by {os.getpid()}")
+
+    q.put(build.build_locked(out, lambda: not os.path.exists(out), compile_to))
+
+
+def test_concurrent_builders_compile_once(tmp_path):
+    """Four processes start a build of the same stale library at once: exactly one compiles,
+    the rest wait on the lock and find the finished file; no temporary file is left behind."""
+    out = str(tmp_path / "lib.so")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_racer, args=(out, q)) for _ in range(4)]
+    for p in procs:
+        p.start()
+    compiled = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert compiled.count(True) == 1
+    assert open(out).read().startswith("built by ")
+    assert sorted(os.listdir(tmp_path)) == ["lib.so", "lib.so.lock"]
+
+
+def test_bench_refuses_wrong_gpu_count():
+    """`python bench.py --gpus 2` without torch.distributed.run exits non-zero at once (before
+    any GPU call), instead of timing one GPU and reporting it as the 2-GPU number."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in r.stderr

@@ -15,8 +15,8 @@ from conftest import read_golden
 pytestmark = pytest.mark.gpu
 
 
-def write_all(gpu, data: bytes, piece: int = 32 * 1024, **kw):
-    st = gpu.MemStore()
+def write_all(gpu, data: bytes, piece: int = 32 * 1024, st=None, **kw):
+    st = gpu.MemStore() if st is None else st
     w = gpu.Writer(st, **kw)
     for i in range(0, len(data), piece):  # io.Copy hands over 32 KiB buffers
         w.write(data[i:i + piece])
@@ -100,6 +100,83 @@ def test_store_put_get(gpu):
     assert st.get(ref) == b"hello"
     with pytest.raises(KeyError):
         st.get(bytes(32))
+
+
+# --------------------------------------------------------------------------------------------
+# gc/gc_test.go:57-131 (TestGC), restated over the C++ Writer + store/mem through the C ABI.
+# gc.Protect / gc.Run (gc/gc.go:38-100) are test harness here (gc is out of scope); split.Protect
+# (split/split.go:306-322) is the library's (bsg_split_protect).
+# --------------------------------------------------------------------------------------------
+def gc_protect(st, root: bytes) -> set:
+    """gc.Protect(ctx, store, k, root, split.Protect): root and everything reachable from it."""
+    keep, todo = set(), [(root, True)]
+    while todo:
+        ref, traverse = todo.pop()
+        if ref in keep:
+            continue
+        keep.add(ref)
+        if traverse:
+            todo.extend(st.protect_children(ref))
+    return keep
+
+
+def gc_run(st, keep: set) -> int:
+    """gc.Run: delete every stored ref not in keep; returns the deletion count (gc.Store)."""
+    deletions = 0
+    for ref in st.refs():
+        if ref not in keep:
+            st.delete(ref)
+            deletions += 1
+    return deletions
+
+
+def test_gc_reference_testgc(gpu):
+    """TestGC exactly: commonsense.txt with split.NewWriter defaults, Protect from its Root,
+    write yubnub.opus, Run, then the store must list exactly the refs it held before yubnub,
+    with at least one deletion."""
+    st = gpu.MemStore()
+    _, root = write_all(gpu, read_golden("commonsense.txt"), st=st)
+    keep = gc_protect(st, root)
+    want = st.refs()
+    _, root2 = write_all(gpu, read_golden("yubnub.opus"), st=st)
+    assert root2 not in keep
+    deletions = gc_run(st, keep)
+    assert deletions > 0, "got 0 deletions during gc.Run"
+    assert st.refs() == want
+    # the invariant TestGC rests on: every blob split.Writer stored is reachable from its Root
+    assert sorted(keep) == want
+
+
+@pytest.mark.parametrize("first,second,bits,fanout,min_size", [
+    ("yubnub.opus", "commonsense.txt", 4, 2, 1024),   # split_test.go's Bits(4)/Fanout(2): deep tree
+    ("commonsense.txt", "yubnub.opus", 8, 2, 1024),
+    ("commonsense.txt", "yubnub.opus", 6, 1, 64),      # Fanout 1: every level closes a node
+    ("splitmix:11:600000", "splitmix:12:300000", 5, 2, 17),
+    ("splitmix:13:2000000", "splitmix:14:500000", 10, 3, 1024),
+])
+def test_gc_reachability_from_root(gpu, first, second, bits, fanout, min_size):
+    """The same invariant at small Bits / Fanout, where the tree has many levels and Root's
+    fold and single-child prune (TreeBuilder.Root, restated) are exercised: the blobs stored by
+    a Writer are exactly those reachable from its Root, and GC after a second stream restores
+    the first stream's set."""
+    from bs_amd.synth import splitmix_bytes
+
+    def data(key):
+        if key.startswith("splitmix:"):
+            _, seed, n = key.split(":")
+            return splitmix_bytes(int(seed), int(n))
+        return read_golden(key)
+
+    st = gpu.MemStore()
+    kw = dict(bits=bits, fanout=fanout, min_size=min_size)
+    _, root = write_all(gpu, data(first), st=st, **kw)
+    keep = gc_protect(st, root)
+    want = st.refs()
+    assert sorted(keep) == want
+    assert gpu.Reader(st, root).read_all() == data(first)
+    write_all(gpu, data(second), st=st, **kw)
+    assert gc_run(st, keep) > 0
+    assert st.refs() == want
 
 
 def test_gc_config1_commonsense(gpu, oracle, table):

@@ -95,6 +95,41 @@ def test_python_and_c_restatements_agree(oracle, table):
             == [(y.offset, y.len, y.level, y.ref) for y in b]
 
 
+# The full ranges split.Bits / split.MinSize accept (split/split.go:137-152 store them
+# unchecked): MinSize 1..63 (a window may span a boundary), Bits 0 (hashsplit default 13) and
+# Bits > 32 (TrailingZeros32 <= 32: never splits, one final chunk of level 0).
+EDGE_PARAMS = [(4, 1), (8, 2), (6, 17), (10, 63), (1, 1), (0, 0), (0, 100), (33, 64), (40, 1),
+               (2**32 - 1, 1024), (32, 1), (31, 5)]
+
+
+def edge_stream(seed: int, n: int) -> bytes:
+    """Random bytes with zero runs and a period-32 stretch (dense candidates: h = 0)."""
+    from bs_amd.synth import splitmix_bytes
+    d = bytearray(splitmix_bytes(seed, n))
+    if n > 3000:
+        d[1000:1700] = bytes(700)
+        pat = splitmix_bytes(seed + 1, 32)
+        d[2000:2900] = (pat * 30)[:900]
+    return bytes(d)
+
+
+@pytest.mark.parametrize("bits,mn", EDGE_PARAMS)
+def test_restatements_agree_on_edge_params(oracle, table, bits, mn):
+    for seed, n in [(21, 5000), (22, 130), (23, 64), (24, 1), (25, 0)]:
+        d = edge_stream(seed + bits % 97 + mn, n)
+        a = oracle.split(table, d, bits=bits, min_size=mn)
+        b = oracle.py_split(table, d, bits=bits, min_size=mn)
+        assert [(int(x["offset"]), int(x["len"]), int(x["level"]), bytes(x["ref"])) for x in a] \
+            == [(y.offset, y.len, y.level, y.ref) for y in b], (bits, mn, n)
+        if n:
+            assert sum(int(x["len"]) for x in a) == n
+        eff_min = mn if mn > 0 else 64
+        assert all(int(x["len"]) >= eff_min for x in a[:-1])
+        if bits > 32:  # never splits: the stream is its final chunk, level 0
+            assert len(a) == (1 if n else 0)
+            assert all(int(x["level"]) == 0 for x in a)
+
+
 def test_multistream_oracle_equals_single(oracle, table):
     from bs_amd.synth import splitmix_array
     arrs = [splitmix_array(100 + i, n) for i, n in enumerate([0, 1, 5000, 70000, 200_000])]
