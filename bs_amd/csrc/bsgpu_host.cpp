@@ -164,7 +164,7 @@ struct bsg_engine {
   int dev = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
-  DevBuf table, streams, strip0, counts, slots, strip_off, partials_a, partials_b, cand, flags,
+  DevBuf table, streams, strip0, counts, hits, slots, strip_off, partials_a, partials_b, cand, flags,
       fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets;
   PinBuf h_streams, h_strip0, h_ctr;
   // Optional snapshot right after selection (streaming pipeline): the counters and every
@@ -220,6 +220,7 @@ struct bsg_engine {
     HCHECK(streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(strip0.ensure(sizeof(uint64_t) * (ns + 1)));
     HCHECK(counts.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
+    HCHECK(hits.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
     HCHECK(slots.ensure(sizeof(uint32_t) * kSlotCap * (strips ? strips : 1)));
     HCHECK(strip_off.ensure(sizeof(uint64_t) * (strips ? strips : 1)));
     HCHECK(partials_a.ensure(sizeof(uint64_t) * prefix_partials_needed(strips)));
@@ -265,6 +266,7 @@ struct bsg_engine {
     sa.table = table.as<uint32_t>();
     sa.p = p;
     sa.counts = counts.as<uint32_t>();
+    sa.hits = hits.as<uint32_t>();
     sa.slots = slots.as<uint32_t>();
     sa.cand_off = strip_off.as<uint64_t>();
     sa.cand = cand.as<uint64_t>();
@@ -272,6 +274,7 @@ struct bsg_engine {
     sa.ctr = dctr;
     mark(0);
     if (strips) HCHECK(dbg("launch_scan", stream, launch_scan(sa, stream, num_cus)));
+    if (strips) HCHECK(dbg("launch_refine", stream, launch_refine(sa, stream, num_cus)));
     mark(1);
 
     PrefixArgs pa{};
@@ -848,7 +851,7 @@ void bsg_engine_destroy(bsg_engine* e) {
   if (!e) return;
   hipSetDevice(e->dev);
   if (e->stream) hipStreamSynchronize(e->stream);
-  DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->slots,
+  DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->hits, &e->slots,
                     &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
                     &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
                     &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets};

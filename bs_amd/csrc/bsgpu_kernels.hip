@@ -124,32 +124,35 @@ __device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t st
   c.count++;
 }
 
-// Exact re-scan of one 64-byte block whose pre-filter hit. The hash at the block start is
-// rebuilt from the 64 bytes before it (the window property: h depends only on those bytes), so
-// the fast loop keeps no state for it, just one bit per block. noinline: its registers stay out
-// of the fast loop's allocation (an inlined re-scan made hipcc spill the fast loop's history).
+// Exact scan of `n` (<= 64) positions starting at a 64-aligned segment offset: the hash before
+// them is rebuilt from the 64 bytes that precede them (the window property: h depends only on
+// those bytes), then each position gets the exact test tz >= bits (equivalent to the fast
+// pass's mask test for bits <= 32; Bits > 32 never splits, hashsplit's tz >= SplitBits with
+// tz <= 32). Loads are whole 64-byte blocks (BSG_READ_SLACK makes the tail block readable).
+// Returns the hash at the last position scanned.
 template <bool WRITE>
-__device__ __noinline__ void slow_block(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                                        const uint8_t* d, const StreamDesc* sd, StripCtx& c,
-                                        uint64_t strip, uint64_t off) {
+__device__ __forceinline__ uint32_t exact_block(const ScanArgs& a, const uint32_t* tab,
+                                                uint32_t lane4, const uint8_t* blk,
+                                                const uint8_t* prev, uint32_t n, StripCtx& c,
+                                                uint64_t strip, uint64_t off) {
   uint32_t w[16], pw[16];
-  load16(d + off, w);
-  if (off >= 64) load16(d + off - 64, pw);
-  else load16(sd->hist, pw);
-  const uint32_t bits = a.p.split_bits;
+  load16(blk, w);
+  load16(prev, pw);
   uint32_t h = 0;
 #pragma unroll
   for (int k = 0; k < 64; ++k) h = rotl1(h) ^ lookup(tab, pw[k >> 2], lane4, k);
+  const uint32_t bits = a.p.split_bits;
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
-    uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
-    uint32_t tout = lookup(tab, pw[k >> 2], lane4, k);
-    h = xor3(rotl1(h), tout, tin);
-    // the exact test (the pre-filter's mask test is equivalent for bits <= 32; Bits > 32 never
-    // splits, hashsplit's tz >= SplitBits with tz <= 32)
-    const uint32_t tz = tz32(h);
-    if (tz >= bits) emit<WRITE>(a, c, strip, off + k, false, tz);
+    if ((uint32_t)k < n) {
+      const uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
+      const uint32_t tout = lookup(tab, pw[k >> 2], lane4, k);
+      h = xor3(rotl1(h), tout, tin);
+      const uint32_t tz = tz32(h);
+      if (tz >= bits) emit<WRITE>(a, c, strip, off + k, false, tz);
+    }
   }
+  return h;
 }
 
 // k_scan / k_compact allocate no LDS but the dynamic table, so the table starts at LDS
@@ -238,23 +241,21 @@ __device__ __forceinline__ void hit_mark(uint32_t (&hits)[N], uint32_t b, bool h
 }
 
 // All full 64-byte blocks of a strip. On entry hA = table values of the 64 bytes before the
-// strip and h = the hash there; on exit hA = those of the last full block. Blocks whose
-// pre-filter hits are only marked here (one bit each in kHitWords words) and re-scanned
-// exactly afterwards in block order, so the candidate order is unchanged and the loop holds
-// nothing but the two histories, two word blocks and the hash.
-template <bool WRITE, bool WIDE>
-__device__ __forceinline__ void scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
-                                                 uint32_t lane4, const uint8_t* d,
-                                                 const StreamDesc* sd, StripCtx& c, uint64_t strip,
-                                                 uint32_t nfull, uint32_t& h, uint32_t (&hA)[64]) {
-  constexpr int kHitWords = (kStrip / 64 + 31) / 32;
+// strip and h = the hash there. Blocks whose pre-filter hits are only marked here (one bit
+// each); k_refine scans them exactly afterwards, in block order, so the fast loop holds
+// nothing but the two histories, two word blocks and the hash (no call, no scratch).
+constexpr int kHitWords = (kStrip / 64 + 31) / 32;
+static_assert(kHitWords == 1, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
+
+template <bool WIDE>
+__device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
+                                                     uint32_t lane4, const uint8_t* base,
+                                                     uint32_t nfull, uint32_t& h,
+                                                     uint32_t (&hA)[64]) {
   const uint32_t mask = a.p.mask;
-  const uint8_t* base = d + c.start;
   uint32_t hB[64];
   uint32_t w[16], wn[16];
-  uint32_t hits[kHitWords];
-#pragma unroll
-  for (int i = 0; i < kHitWords; ++i) hits[i] = 0;
+  uint32_t hits[1] = {0};
   scan_load16(base, w);
   lookup64(tab, w, hB, lane4);                       // hB = block 0
   uint32_t b = 0;
@@ -276,14 +277,7 @@ __device__ __forceinline__ void scan_full_blocks(const ScanArgs& a, const uint32
 #pragma unroll
     for (int k = 0; k < 64; ++k) hA[k] = hB[k];
   }
-#pragma unroll
-  for (int i = 0; i < kHitWords; ++i) {
-    while (hits[i]) {
-      const uint32_t bb = 32u * i + (uint32_t)__builtin_ctz(hits[i]);
-      hits[i] &= hits[i] - 1;
-      slow_block<WRITE>(a, tab, lane4, d, sd, c, strip, c.start + 64ull * bb);
-    }
-  }
+  return hits[0];
 }
 
 // strip0 (the streams' first strips) cached in LDS after the table, when it fits: the stream
@@ -298,29 +292,46 @@ __device__ __forceinline__ lds_u64p cache_strip0(uint32_t* lds_after, const Scan
   return (lds_u64p)(s0);  // generic -> LDS address space
 }
 
-template <bool WRITE>
-__device__ __forceinline__ uint32_t scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                               uint64_t strip, uint64_t wbase, lds_u64p s0 = nullptr) {
-  StripCtx c;
+// Where a strip lies: its stream (binary search over the streams' first strips) and segment.
+struct StripLoc {
+  uint32_t stream;
+  uint64_t start;     // segment offset of the strip
+  uint32_t len;       // bytes in the strip
+  bool last;          // the segment's last strip
+};
+
+__device__ __forceinline__ StripLoc locate(const ScanArgs& a, uint64_t strip, lds_u64p s0) {
+  StripLoc l;
   uint64_t first;
   if (s0) {
-    c.stream = find_stream(s0, a.nstreams, strip);
-    first = s0[c.stream];
+    l.stream = find_stream(s0, a.nstreams, strip);
+    first = s0[l.stream];
   } else {
-    c.stream = find_stream(a.strip0, a.nstreams, strip);
-    first = a.strip0[c.stream];
+    l.stream = find_stream(a.strip0, a.nstreams, strip);
+    first = a.strip0[l.stream];
   }
-  const StreamDesc* sd = a.streams + c.stream;
-  const uint64_t seglen = sd->len;
-  c.start = (strip - first) * (uint64_t)kStrip;
-  c.count = 0;
-  c.wbase = wbase;
-  c.seg_base = sd->seg_base;
-  const uint32_t len = (uint32_t)min((uint64_t)kStrip, seglen - c.start);
-  const uint8_t* d = a.data + sd->data_off;
+  const uint64_t seglen = a.streams[l.stream].len;
+  l.start = (strip - first) * (uint64_t)kStrip;
+  l.len = (uint32_t)min((uint64_t)kStrip, seglen - l.start);
+  l.last = l.start + l.len == seglen;
+  return l;
+}
 
+// Marker in counts[] left by k_scan for k_refine: the strip has pre-filter hits or a tail.
+constexpr uint32_t kNeedRefine = 0xffffffffu;
+
+// Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
+// hit bit per block whose pre-filter fires. Writes hits[strip], and counts[strip] = 0, or
+// kNeedRefine when k_refine has exact work (hit blocks, the segment's < 64-byte tail, or the
+// final chunk's flush).
+template <bool WIDE>
+__device__ __forceinline__ void scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
+                                           uint64_t strip, lds_u64p s0) {
+  const StripLoc l = locate(a, strip, s0);
+  const StreamDesc* sd = a.streams + l.stream;
+  const uint8_t* d = a.data + sd->data_off;
   uint32_t w[16];
-  if (c.start >= 64) load16(d + c.start - 64, w);
+  if (l.start >= 64) load16(d + l.start - 64, w);
   else load16(sd->hist, w);
   uint32_t hist[64];
   uint32_t h = 0;
@@ -330,35 +341,54 @@ __device__ __forceinline__ uint32_t scan_strip(const ScanArgs& a, const uint32_t
     h = rotl1(h) ^ t;
     hist[k] = t;
   }
+  const uint32_t nfull = l.len >> 6;
+  uint32_t hits = 0;
+  if (nfull) hits = scan_full_blocks<WIDE>(a, tab, lane4, d + l.start, nfull, h, hist);
+  const bool tail = (l.len & 63u) != 0 || (l.last && sd->finalize);
+  a.hits[strip] = hits;
+  a.counts[strip] = (hits || tail) ? kNeedRefine : 0u;
+}
 
-  const uint32_t nfull = len >> 6;
-  if (nfull) {
-    if (a.p.split_bits >= 16) scan_full_blocks<WRITE, true>(a, tab, lane4, d, sd, c, strip, nfull, h, hist);
-    else scan_full_blocks<WRITE, false>(a, tab, lane4, d, sd, c, strip, nfull, h, hist);
+// Exact candidates of one strip flagged by the fast pass, in position order: its hit blocks,
+// then the segment's tail (< 64 bytes), then Splitter.Close()'s flush of the final chunk (a
+// forced candidate at the last byte, level from the same check). WRITE = false: the first
+// kSlotCap into the strip's slots; true: all of them straight into the candidate list at wbase.
+template <bool WRITE>
+__device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32_t* tab,
+                                                 uint32_t lane4, uint64_t strip, uint64_t wbase,
+                                                 lds_u64p s0) {
+  const StripLoc l = locate(a, strip, s0);
+  const StreamDesc* sd = a.streams + l.stream;
+  const uint8_t* d = a.data + sd->data_off;
+  StripCtx c;
+  c.stream = l.stream;
+  c.start = l.start;
+  c.count = 0;
+  c.wbase = wbase;
+  c.seg_base = sd->seg_base;
+  uint32_t hits = a.hits[strip];
+  while (hits) {
+    const uint64_t off = l.start + 64ull * (uint32_t)__builtin_ctz(hits);
+    hits &= hits - 1;
+    exact_block<WRITE>(a, tab, lane4, d + off, off >= 64 ? d + off - 64 : sd->hist, 64u, c,
+                       strip, off);
   }
-
-  const uint32_t rem = len & 63u;
-  if (rem) {  // tail of the segment: byte loads, never past the end
-    const uint64_t off = c.start + 64ull * nfull;
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-      if ((uint32_t)k < rem) {
-        uint32_t byte = d[off + k];
-        uint32_t t = lds_at(tab, (byte << 8) | lane4);
-        h = xor3(rotl1(h), hist[k], t);
-        hist[k] = t;
-        const uint32_t tz = tz32(h);
-        if (tz >= a.p.split_bits) emit<WRITE>(a, c, strip, off + k, false, tz);
-      }
-    }
-  }
-  if (c.start + len == seglen && sd->finalize) {
-    // Splitter.Close(): the remainder becomes the final chunk; level from the same check.
-    emit<WRITE>(a, c, strip, seglen - 1, true, tz32(h));
+  const uint32_t rem = l.len & 63u;
+  const bool flush = l.last && sd->finalize;
+  if (rem || flush) {
+    // the hash entering the tail (or, with no tail, at the segment's last byte) is rebuilt
+    // from the 64 bytes before the tail's 64-aligned start
+    const uint64_t off = l.start + (l.len & ~63u);
+    const uint32_t h = exact_block<WRITE>(a, tab, lane4, d + off,
+                                          off >= 64 ? d + off - 64 : sd->hist, rem, c, strip, off);
+    if (flush) emit<WRITE>(a, c, strip, l.start + l.len - 1, true, tz32(h));
   }
   return c.count;
 }
 
+// WIDE (split_bits >= 16, the packed 16-bit pre-filter) and the narrow form are separate
+// kernels, so each holds one copy of the fast loop and its registers.
+template <bool WIDE>
 __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
   if (!table_at_lds0(tab)) {
@@ -371,8 +401,27 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
-    if (strip < a.nstrips) {
-      const uint32_t n = scan_strip<false>(a, tab, lane4, strip, 0, s0);
+    if (strip < a.nstrips) scan_strip<WIDE>(a, tab, lane4, strip, s0);
+  }
+}
+
+// Exact pass over the strips k_scan flagged (a few percent of them on random data at the
+// default Bits 16; all of them on degenerate data): exact counts into counts[], the first
+// kSlotCap candidates into the strip's slots; strips with more are left to k_rescan.
+__global__ __launch_bounds__(kScanWG, 2) void k_refine(ScanArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+  if (!table_at_lds0(tab)) {
+    if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
+    return;
+  }
+  load_table(tab, a.table);
+  const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
+  __syncthreads();
+  const uint32_t lane4 = (threadIdx.x & 63u) << 2;
+  for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
+    const uint64_t strip = g * kScanWG + threadIdx.x;
+    if (strip < a.nstrips && a.counts[strip] == kNeedRefine) {
+      const uint32_t n = refine_strip<false>(a, tab, lane4, strip, 0, s0);
       a.counts[strip] = n;
       if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
     }
@@ -425,7 +474,7 @@ __global__ __launch_bounds__(kScanWG, 2) void k_rescan(ScanArgs a) {
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
     const uint32_t cnt = strip < a.nstrips ? a.counts[strip] : 0u;
-    if (cnt > (uint32_t)kSlotCap) scan_strip<true>(a, tab, lane4, strip, a.cand_off[strip]);
+    if (cnt > (uint32_t)kSlotCap) refine_strip<true>(a, tab, lane4, strip, a.cand_off[strip], nullptr);
   }
 }
 
@@ -1321,7 +1370,17 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
   const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
   const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_scan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
+  if (a.p.split_bits >= 16)
+    hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
+  else
+    hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus) {
+  const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
+  const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_refine, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
   return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@ struct ScanArgs {
   const uint32_t* table;    // 256 buzhash32 entries
   Params p;
   uint32_t* counts;         // [nstrips]
+  uint32_t* hits;           // [nstrips] k_scan's pre-filter hit mask, one bit per 64-byte block
   uint32_t* slots;          // [nstrips * kSlotCap]
   const uint64_t* cand_off; // [nstrips] exclusive candidate offsets (compact)
   uint64_t* cand;           // [cand_cap]
@@ -94,6 +95,7 @@ struct BlobShaArgs {
 };
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus);
+hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus);
 hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus);
 uint64_t prefix_partials_needed(uint64_t n_bound);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s);
