@@ -164,7 +164,7 @@ struct bsg_engine {
   int dev = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
-  DevBuf table, streams, strip0, counts, hits, slots, strip_off, partials_a, partials_b, cand, flags,
+  DevBuf table, streams, strip0, counts, refine, slots, strip_off, partials_a, partials_b, cand, flags,
       fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets;
   PinBuf h_streams, h_strip0, h_ctr;
   // Optional snapshot right after selection (streaming pipeline): the counters and every
@@ -220,7 +220,7 @@ struct bsg_engine {
     HCHECK(streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(strip0.ensure(sizeof(uint64_t) * (ns + 1)));
     HCHECK(counts.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
-    HCHECK(hits.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
+    HCHECK(refine.ensure(sizeof(uint64_t) * (strips ? strips : 1)));
     HCHECK(slots.ensure(sizeof(uint32_t) * kSlotCap * (strips ? strips : 1)));
     HCHECK(strip_off.ensure(sizeof(uint64_t) * (strips ? strips : 1)));
     HCHECK(partials_a.ensure(sizeof(uint64_t) * prefix_partials_needed(strips)));
@@ -266,7 +266,7 @@ struct bsg_engine {
     sa.table = table.as<uint32_t>();
     sa.p = p;
     sa.counts = counts.as<uint32_t>();
-    sa.hits = hits.as<uint32_t>();
+    sa.refine = refine.as<uint64_t>();
     sa.slots = slots.as<uint32_t>();
     sa.cand_off = strip_off.as<uint64_t>();
     sa.cand = cand.as<uint64_t>();
@@ -851,7 +851,7 @@ void bsg_engine_destroy(bsg_engine* e) {
   if (!e) return;
   hipSetDevice(e->dev);
   if (e->stream) hipStreamSynchronize(e->stream);
-  DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->hits, &e->slots,
+  DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->refine, &e->slots,
                     &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
                     &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
                     &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets};

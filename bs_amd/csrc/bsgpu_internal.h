@@ -108,7 +108,8 @@ struct Counters {
   uint64_t lane_end_rt;        // latest s_memrealtime at which a wave left per-lane mode
   uint64_t nlong_grp;          // long jobs on solo / kGroup tickets; the rest of the long list
   uint64_t tickets_grp;        //   runs on pair tickets (kPairGroup jobs, one lane pair each)
-  uint64_t pad_[2];
+  uint64_t nrefine;            // strips k_scan listed for the exact pass (k_refine)
+  uint64_t pad_[1];
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 

@@ -254,26 +254,30 @@ __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const ui
                                                      uint32_t (&hA)[64]) {
   const uint32_t mask = a.p.mask;
   uint32_t hB[64];
-  uint32_t w[16], wn[16];
+  // Blocks are loaded in pairs, the two 64-byte halves of one 128-byte line back to back, so
+  // the line is fetched once: loaded one block apart, the second half often found its line
+  // evicted from L2 and fetched it again (k_scan read 1.5x its input on configs[1]).
+  uint32_t w0[16], w1[16], n0[16], n1[16];
   uint32_t hits[1] = {0};
-  scan_load16(base, w);
-  lookup64(tab, w, hB, lane4);                       // hB = block 0
+  scan_load16(base, w0);
+  scan_load16(base + 64ull * min(1u, nfull - 1), w1);  // (clamped, branch-free)
+  lookup64(tab, w0, hB, lane4);                         // hB = block 0
   uint32_t b = 0;
-  scan_load16(base + 64ull * min(1u, nfull - 1), wn);  // block 1 (clamped, branch-free)
   for (; b + 1 < nfull; b += 2) {
+    scan_load16(base + 64ull * min(b + 2, nfull - 1), n0);  // the next line
+    scan_load16(base + 64ull * min(b + 3, nfull - 1), n1);
     // block b: out-going hA, in-coming hB; looks up block b+1 into hA
-#pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = wn[i];
-    scan_load16(base + 64ull * min(b + 2, nfull - 1), wn);
-    hit_mark(hits, b, chain64<WIDE, true>(tab, w, hA, hB, h, lane4, mask));
+    hit_mark(hits, b, chain64<WIDE, true>(tab, w1, hA, hB, h, lane4, mask));
     // block b+1: out-going hB, in-coming hA; looks up block b+2 into hB
+    hit_mark(hits, b + 1, chain64<WIDE, true>(tab, n0, hB, hA, h, lane4, mask));
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = wn[i];
-    scan_load16(base + 64ull * min(b + 3, nfull - 1), wn);
-    hit_mark(hits, b + 1, chain64<WIDE, true>(tab, w, hB, hA, h, lane4, mask));
+    for (int i = 0; i < 16; ++i) {
+      w0[i] = n0[i];
+      w1[i] = n1[i];
+    }
   }
   if (b < nfull) {  // odd block count: the last block, then its values back into hA
-    hit_mark(hits, b, chain64<WIDE, false>(tab, w, hA, hB, h, lane4, mask));
+    hit_mark(hits, b, chain64<WIDE, false>(tab, w1, hA, hB, h, lane4, mask));
 #pragma unroll
     for (int k = 0; k < 64; ++k) hA[k] = hB[k];
   }
@@ -317,16 +321,13 @@ __device__ __forceinline__ StripLoc locate(const ScanArgs& a, uint64_t strip, ld
   return l;
 }
 
-// Marker in counts[] left by k_scan for k_refine: the strip has pre-filter hits or a tail.
-constexpr uint32_t kNeedRefine = 0xffffffffu;
-
 // Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
-// hit bit per block whose pre-filter fires. Writes hits[strip], and counts[strip] = 0, or
-// kNeedRefine when k_refine has exact work (hit blocks, the segment's < 64-byte tail, or the
-// final chunk's flush).
+// hit bit per block whose pre-filter fires. Writes counts[strip] = 0 and returns whether
+// k_refine has exact work for the strip (hit blocks, the segment's < 64-byte tail, or the
+// final chunk's flush), with the hit mask in *hits_out.
 template <bool WIDE>
-__device__ __forceinline__ void scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                                           uint64_t strip, lds_u64p s0) {
+__device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
+                                           uint64_t strip, lds_u64p s0, uint32_t* hits_out) {
   const StripLoc l = locate(a, strip, s0);
   const StreamDesc* sd = a.streams + l.stream;
   const uint8_t* d = a.data + sd->data_off;
@@ -345,8 +346,32 @@ __device__ __forceinline__ void scan_strip(const ScanArgs& a, const uint32_t* ta
   uint32_t hits = 0;
   if (nfull) hits = scan_full_blocks<WIDE>(a, tab, lane4, d + l.start, nfull, h, hist);
   const bool tail = (l.len & 63u) != 0 || (l.last && sd->finalize);
-  a.hits[strip] = hits;
-  a.counts[strip] = (hits || tail) ? kNeedRefine : 0u;
+  a.counts[strip] = 0u;
+  *hits_out = hits;
+  return hits || tail;
+}
+
+// Appends the flagged strips of a wave to the refine list, one atomic per wave: entry =
+// strip << 32 | hit mask.
+__device__ __forceinline__ void refine_append(const ScanArgs& a, bool flag, uint64_t strip,
+                                              uint32_t hits) {
+  const uint64_t m = __ballot(flag);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  uint32_t base_lo = 0, base_hi = 0;
+  if (lane == leader) {
+    const uint64_t b = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->nrefine),
+                                 (unsigned long long)__builtin_popcountll(m));
+    base_lo = (uint32_t)b;
+    base_hi = (uint32_t)(b >> 32);
+  }
+  const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)base_hi, (int)leader) << 32) |
+                        (uint32_t)__shfl((int)base_lo, (int)leader);
+  if (flag) {
+    const uint64_t below = m & ((1ull << lane) - 1ull);
+    a.refine[base + (uint64_t)__builtin_popcountll(below)] = (strip << 32) | hits;
+  }
 }
 
 // Exact candidates of one strip flagged by the fast pass, in position order: its hit blocks,
@@ -355,8 +380,8 @@ __device__ __forceinline__ void scan_strip(const ScanArgs& a, const uint32_t* ta
 // kSlotCap into the strip's slots; true: all of them straight into the candidate list at wbase.
 template <bool WRITE>
 __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32_t* tab,
-                                                 uint32_t lane4, uint64_t strip, uint64_t wbase,
-                                                 lds_u64p s0) {
+                                                 uint32_t lane4, uint64_t strip, uint32_t hits,
+                                                 uint64_t wbase, lds_u64p s0) {
   const StripLoc l = locate(a, strip, s0);
   const StreamDesc* sd = a.streams + l.stream;
   const uint8_t* d = a.data + sd->data_off;
@@ -366,7 +391,6 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
   c.count = 0;
   c.wbase = wbase;
   c.seg_base = sd->seg_base;
-  uint32_t hits = a.hits[strip];
   while (hits) {
     const uint64_t off = l.start + 64ull * (uint32_t)__builtin_ctz(hits);
     hits &= hits - 1;
@@ -401,13 +425,17 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
-    if (strip < a.nstrips) scan_strip<WIDE>(a, tab, lane4, strip, s0);
+    bool flag = false;
+    uint32_t hits = 0;
+    if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, s0, &hits);
+    refine_append(a, flag, strip, hits);
   }
 }
 
-// Exact pass over the strips k_scan flagged (a few percent of them on random data at the
-// default Bits 16; all of them on degenerate data): exact counts into counts[], the first
-// kSlotCap candidates into the strip's slots; strips with more are left to k_rescan.
+// Exact pass over the strips k_scan listed (a few percent of them on random data at the
+// default Bits 16; all of them on degenerate data), one per lane from the compacted list, so
+// the waves are full: exact counts into counts[], the first kSlotCap candidates into the
+// strip's slots; strips with more are left to k_rescan.
 __global__ __launch_bounds__(kScanWG, 2) void k_refine(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
   if (!table_at_lds0(tab)) {
@@ -418,13 +446,14 @@ __global__ __launch_bounds__(kScanWG, 2) void k_refine(ScanArgs a) {
   const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
-  for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
-    const uint64_t strip = g * kScanWG + threadIdx.x;
-    if (strip < a.nstrips && a.counts[strip] == kNeedRefine) {
-      const uint32_t n = refine_strip<false>(a, tab, lane4, strip, 0, s0);
-      a.counts[strip] = n;
-      if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
-    }
+  const uint64_t nref = a.ctr->nrefine;
+  for (uint64_t i = (uint64_t)blockIdx.x * kScanWG + threadIdx.x; i < nref;
+       i += (uint64_t)gridDim.x * kScanWG) {
+    const uint64_t e = a.refine[i];
+    const uint64_t strip = e >> 32;
+    const uint32_t n = refine_strip<false>(a, tab, lane4, strip, (uint32_t)e, 0, s0);
+    a.counts[strip] = n;
+    if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
   }
 }
 
@@ -471,10 +500,13 @@ __global__ __launch_bounds__(kScanWG, 2) void k_rescan(ScanArgs a) {
   load_table(tab, a.table);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
-  for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
-    const uint64_t strip = g * kScanWG + threadIdx.x;
-    const uint32_t cnt = strip < a.nstrips ? a.counts[strip] : 0u;
-    if (cnt > (uint32_t)kSlotCap) refine_strip<true>(a, tab, lane4, strip, a.cand_off[strip], nullptr);
+  const uint64_t nref = a.ctr->nrefine;
+  for (uint64_t i = (uint64_t)blockIdx.x * kScanWG + threadIdx.x; i < nref;
+       i += (uint64_t)gridDim.x * kScanWG) {
+    const uint64_t e = a.refine[i];
+    const uint64_t strip = e >> 32;
+    if (a.counts[strip] > (uint32_t)kSlotCap)
+      refine_strip<true>(a, tab, lane4, strip, (uint32_t)e, a.cand_off[strip], nullptr);
   }
 }
 

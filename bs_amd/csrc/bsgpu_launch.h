@@ -16,7 +16,8 @@ struct ScanArgs {
   const uint32_t* table;    // 256 buzhash32 entries
   Params p;
   uint32_t* counts;         // [nstrips]
-  uint32_t* hits;           // [nstrips] k_scan's pre-filter hit mask, one bit per 64-byte block
+  uint64_t* refine;         // [nstrips] strips k_refine must scan exactly: strip << 32 | the
+                            // fast pass's hit mask (one bit per 64-byte block); ctr->nrefine
   uint32_t* slots;          // [nstrips * kSlotCap]
   const uint64_t* cand_off; // [nstrips] exclusive candidate offsets (compact)
   uint64_t* cand;           // [cand_cap]

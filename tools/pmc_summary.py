@@ -9,11 +9,13 @@ Writes profiles/<round>_kernel_stats.csv (verbatim copy) and profiles/<round>_pm
   per kernel: launches, FETCH_SIZE / WRITE_SIZE per launch (KiB, raw) and corrected HBM bytes.
 
 Correction (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE counts
-exactly half the bytes of a wide coalesced streaming read, so FETCH bytes are doubled for the
-kernels whose loads are wide contiguous per-wave reads (k_sha: a wave reads 64 consecutive
-64-byte blocks, 16 B per lane per load). Other kernels keep the raw value and are flagged
-"uncalibrated" (k_scan's loads are 16 B per lane from 64 different 2 KiB strips). WRITE_SIZE is
-exact for the calibrating case (k_fill_splitmix writes 1 GiB and reports 1048576 KiB).
+exactly half the bytes of a wide coalesced streaming read (128-byte requests tallied at 64), so
+FETCH bytes are doubled for the kernels whose loads are 16 B per lane (k_sha, k_sha_blobs,
+k_scan, k_refine). k_scan's pattern (each lane streams its own 2 KiB strip, 64 B per block) is
+also calibrated on its own: tools/ubench/scan_calib reads a known byte count with exactly that
+pattern (k_strips) and with the guide's coalesced pattern (k_coalesced); --calib <dir> reads
+that run's FETCH_SIZE pass and reports, per kernel of the strip pattern, its FETCH per
+algorithmic byte relative to k_strips'. WRITE_SIZE is exact for 16-B streaming stores.
 """
 import argparse
 import collections
@@ -23,7 +25,10 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FETCH_X2 = {"bsg::k_sha(bsg::ShaArgs)", "bsg::k_sha_blobs(bsg::BlobShaArgs)"}
+FETCH_X2 = {"bsg::k_sha(bsg::ShaArgs)", "bsg::k_sha_blobs(bsg::BlobShaArgs)",
+            "void bsg::k_scan<true>(bsg::ScanArgs)", "void bsg::k_scan<false>(bsg::ScanArgs)",
+            "bsg::k_refine(bsg::ScanArgs)"}
+STRIP_PATTERN = {"void bsg::k_scan<true>(bsg::ScanArgs)", "void bsg::k_scan<false>(bsg::ScanArgs)"}
 
 
 def _counters(path):
@@ -39,7 +44,19 @@ def main():
     ap.add_argument("--round", required=True)
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--workload", default="configs[1]: 1 GiB random stream per GPU")
+    ap.add_argument("--bytes", type=float, default=float(1 << 30),
+                    help="algorithmic input bytes per launch (stream bytes of the batch)")
+    ap.add_argument("--calib", default=None, help="scan_calib FETCH_SIZE run directory")
     a = ap.parse_args()
+    calib = None
+    if a.calib:
+        cf = _counters(os.path.join(a.calib, "run_counter_collection.csv"))
+        strips = [v for k, v in cf.items() if k.startswith("k_strips")][0][0]
+        coal = [v for k, v in cf.items() if k.startswith("k_coalesced")][0][0]
+        alg = float(1 << 30) + ((1 << 30) // 2048 - 1) * 64.0  # strips + warm-up blocks
+        calib = {"k_strips_fetch_kib": strips, "k_coalesced_fetch_kib": coal,
+                 "k_strips_fetch_per_byte": strips * 1024 / alg,
+                 "k_coalesced_fetch_per_byte": coal * 1024 / float(1 << 30)}
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     stats = os.path.join(a.src, "prof_trace", "run_kernel_stats.csv")
@@ -60,12 +77,19 @@ def main():
         kernels[name] = {
             "launches": len(fetch.get(name, [])),
             "fetch_kib_raw": fk, "write_kib_raw": wk,
-            "fetch_correction": "x2 (wide coalesced reads, gfx950)" if x2 else "uncalibrated (raw)",
+            "fetch_correction": "x2 (16 B/lane reads, gfx950)" if x2 else "uncalibrated (raw)",
             "hbm_bytes_per_launch": fb + wb,
+            "read_over_algorithmic": fb / a.bytes,
+            "write_bytes_per_launch": wb,
             "avg_ns": avg_ns.get(name),
         }
-    doc = {"round": a.round, "workload": a.workload, "source": "rocprofv3 --pmc FETCH_SIZE / "
-           "WRITE_SIZE, separate passes, bench.py --steps 1 --warmup 0", "kernels": kernels}
+        if calib and name in STRIP_PATTERN:
+            kernels[name]["fetch_vs_strip_calibration"] = (fk * 1024 / a.bytes) / \
+                calib["k_strips_fetch_per_byte"]
+    doc = {"round": a.round, "workload": a.workload, "algorithmic_bytes_per_launch": a.bytes,
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py "
+                     "--steps 1 --warmup 0", "strip_pattern_calibration": calib,
+           "kernels": kernels}
     with open(os.path.join(out, f"{a.round}_pmc.json"), "w") as f:
         json.dump(doc, f, indent=1)
     for n, k in kernels.items():
