@@ -8,11 +8,15 @@
 // nodes are PutProto'd and whose chunks are Put. Root() folds the open levels and prunes
 // single-child roots. Parity of Root with Go is unpinned (the module's source is not in the
 // reference tree), chunk boundaries and refs are pinned by the tests.
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 
 #include "../../include/bs_split.hpp"
@@ -54,7 +58,7 @@ Status MemStore::Get(const Ref& ref, std::vector<uint8_t>* out) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = blobs_.find(ref);
   if (it == blobs_.end()) return Status::Err(kNotFound, "not found");
-  *out = it->second;
+  out->assign(it->second.bytes(), it->second.bytes() + it->second.size);
   return Status::Ok();
 }
 
@@ -70,7 +74,18 @@ Status MemStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool*
   std::lock_guard<std::mutex> g(mu_);
   auto it = blobs_.find(ref);
   bool add = it == blobs_.end();
-  if (add) blobs_.emplace(ref, std::vector<uint8_t>(data, data + n));
+  if (add) {  // a caller's buffer: keep a copy
+    std::shared_ptr<uint8_t> own(new uint8_t[n ? n : 1], std::default_delete<uint8_t[]>());
+    if (n) std::memcpy(own.get(), data, n);
+    blobs_.emplace(ref, Blob{std::move(own), n});
+  }
+  if (added) *added = add;
+  return Status::Ok();
+}
+
+Status MemStore::PutBlob(const Ref& ref, const Blob& b, bool* added) {  // mem.go:62-76
+  std::lock_guard<std::mutex> g(mu_);
+  const bool add = blobs_.emplace(ref, b).second;
   if (added) *added = add;
   return Status::Ok();
 }
@@ -397,36 +412,110 @@ Status Writer::Drain() {
     const bsg_chunk& c = drained_[i];
     if (c.offset != emitted_ || c.offset + c.len > end_)
       return Status::Err(BSG_EDEVICE, "chunk records out of order");
-    // the chunk's bytes: in place if one piece holds them, else gathered into span_
-    const uint8_t* bytes = nullptr;
+    // the chunk's bytes: an alias of the piece that holds them, or (a chunk across pieces)
+    // gathered into a buffer of its own
+    Blob blob;
+    blob.size = c.len;
     uint64_t skip = c.offset - base_;
     size_t k = 0;
-    while (skip >= pieces_[k].size()) skip -= pieces_[k++].size();
-    if (skip + c.len <= pieces_[k].size()) {
-      bytes = pieces_[k].data() + skip;
+    while (skip >= pieces_[k].size) skip -= pieces_[k++].size;
+    if (skip + c.len <= pieces_[k].size) {
+      blob.data = std::shared_ptr<const uint8_t>(pieces_[k].buf, pieces_[k].buf.get() + skip);
     } else {
-      span_.resize(c.len);
+      std::shared_ptr<uint8_t> own(new uint8_t[c.len], std::default_delete<uint8_t[]>());
       uint64_t done = 0;
       for (; done < c.len; ++k, skip = 0) {
-        const uint64_t take = std::min<uint64_t>(c.len - done, pieces_[k].size() - skip);
-        std::memcpy(span_.data() + done, pieces_[k].data() + skip, take);
+        const uint64_t take = std::min<uint64_t>(c.len - done, pieces_[k].size - skip);
+        std::memcpy(own.get() + done, pieces_[k].buf.get() + skip, take);
         done += take;
       }
-      bytes = span_.data();
+      blob.data = std::move(own);
     }
     Ref ref;
     std::memcpy(ref.data(), c.ref, 32);
     bool added;
-    Status s = rp_ ? rp_->PutWithRef(ref, bytes, c.len, &added)  // GPU ref, no re-hash
-                   : st_->Put(bytes, c.len, &ref, &added);       // store computes the ref
+    Status s = rp_ ? rp_->PutBlob(ref, blob, &added)                // GPU ref, no re-hash
+                   : st_->Put(blob.bytes(), c.len, &ref, &added);  // store computes the ref
     if (!s.ok()) return s;
     emitted_ += c.len;
-    while (!pieces_.empty() && base_ + pieces_.front().size() <= emitted_) {  // fully emitted
-      base_ += pieces_.front().size();
+    while (!pieces_.empty() && base_ + pieces_.front().size <= emitted_) {  // fully emitted
+      base_ += pieces_.front().size;
       pieces_.pop_front();
     }
     s = Add(ref, c.len, c.level / opt_.fanout);  // split/split.go:86
     if (!s.ok()) return s;
+  }
+  return Status::Ok();
+}
+
+// A piece buffer. Large ones are their own anonymous mapping with transparent huge pages
+// requested: they are written once, kept by the store, and a fresh 4 KiB-page heap buffer
+// costs a page fault per 4 KiB on its first write (the largest cost of a Write before).
+static std::shared_ptr<uint8_t> alloc_piece(size_t n) {
+  constexpr size_t kHuge = 2ull << 20;
+  if (n >= kHuge) {
+    const size_t len = (n + kHuge - 1) & ~(kHuge - 1);
+    void* m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m != MAP_FAILED) {
+      (void)::madvise(m, len, MADV_HUGEPAGE);
+      return std::shared_ptr<uint8_t>(static_cast<uint8_t*>(m),
+                                      [len](uint8_t* q) { ::munmap(q, len); });
+    }
+  }
+  return std::shared_ptr<uint8_t>(new (std::nothrow) uint8_t[n ? n : 1],
+                                  std::default_delete<uint8_t[]>());
+}
+
+// Host threads for a large Write's copies (as bsg_write's own: BSG_COPY_THREADS, default 8).
+static unsigned writer_threads() {
+  static unsigned v = 0;
+  if (!v) {
+    const char* e = std::getenv("BSG_COPY_THREADS");
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    v = std::max(1u, std::min(hw, e ? (unsigned)std::max(1, std::atoi(e)) : 8u));
+  }
+  return v;
+}
+
+// Copies p[0..n) into dst (the Writer's piece) and, through the zero-copy window, into the
+// context's pinned staging: one read of the caller's bytes feeds both copies (each thread
+// copies a 64 KiB slice into the piece, then from there, still in cache, into the window), on
+// up to writer_threads() threads for large Writes.
+Status Writer::Copy(const uint8_t* p, size_t n, uint8_t* dst) {
+  size_t done = 0;
+  while (done < n) {
+    uint8_t* win = nullptr;
+    size_t cap = 0;
+    int rc = bsg_write_window(ctx_, &win, &cap);
+    if (rc) return Status::Err(rc, std::string("bsg_write_window: ") + bsg_errstr(rc));
+    const size_t k = std::min(cap, n - done);
+    const uint8_t* src = p + done;
+    uint8_t* d1 = dst + done;
+    auto work = [=](size_t lo, size_t hi) {
+      constexpr size_t kSlice = 64 << 10;
+      for (size_t o = lo; o < hi; o += kSlice) {
+        const size_t m = std::min(kSlice, hi - o);
+        std::memcpy(d1 + o, src + o, m);
+        std::memcpy(win + o, d1 + o, m);
+      }
+    };
+    constexpr size_t kPerThread = 2ull << 20;
+    const unsigned nt = (unsigned)std::min<size_t>(writer_threads(), k / kPerThread);
+    if (nt <= 1) {
+      work(0, k);
+    } else {
+      std::vector<std::thread> th;
+      const size_t per = ((k + nt - 1) / nt + 4095) & ~(size_t)4095;
+      for (unsigned t = 0; t < nt; ++t) {
+        const size_t lo = t * per;
+        if (lo >= k) break;
+        th.emplace_back(work, lo, std::min(k, lo + per));
+      }
+      for (auto& x : th) x.join();
+    }
+    rc = bsg_write_commit(ctx_, k);
+    if (rc) return Status::Err(rc, std::string("bsg_write_commit: ") + bsg_errstr(rc));
+    done += k;
   }
   return Status::Ok();
 }
@@ -436,11 +525,13 @@ Status Writer::Write(const uint8_t* p, size_t n, size_t* written) {
   if (closed_) return Status::Err(BSG_ESTATE, "write after close");
   if (!sticky_.ok()) return sticky_;
   if (n) {
-    pieces_.emplace_back(p, p + n);
+    Piece piece{alloc_piece(n), n};
+    if (!piece.buf) return sticky_ = Status::Err(BSG_ENOMEM, "piece allocation");
+    Status s = Copy(p, n, piece.buf.get());
+    if (!s.ok()) return sticky_ = s;
+    pieces_.push_back(std::move(piece));
     end_ += n;
   }
-  int rc = bsg_write(ctx_, p, n);
-  if (rc) return sticky_ = Status::Err(rc, std::string("bsg_write: ") + bsg_errstr(rc));
   Status s = Drain();
   if (!s.ok()) return sticky_ = s;
   if (written) *written = n;

@@ -56,10 +56,25 @@ class Store {
   virtual Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) = 0;
 };
 
+// A blob's bytes with shared ownership: `data` points into memory kept alive by the
+// shared_ptr (an aliasing pointer into a larger buffer, e.g. a Writer's input piece), so a store
+// can retain a chunk without copying it, as store/mem retains the caller's slice
+// (store/mem/mem.go:71). The bytes must never change afterwards.
+struct Blob {
+  std::shared_ptr<const uint8_t> data;
+  size_t size = 0;
+  const uint8_t* bytes() const { return data.get(); }
+};
+
 class RefPutter {
  public:
   virtual ~RefPutter() = default;
   virtual Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) = 0;
+  // The same with shared ownership of the bytes: a store that retains blobs in memory keeps
+  // the Blob itself (no copy); others just read it.
+  virtual Status PutBlob(const Ref& ref, const Blob& b, bool* added) {
+    return PutWithRef(ref, b.bytes(), b.size, added);
+  }
 };
 
 // Batched/one-off SHA-256 of host bytes on the GPU (bsg_hasher: persistent device buffers +
@@ -88,6 +103,8 @@ class MemStore : public Store, public RefPutter {
   Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) override;
   Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
   Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
+  // Keeps b itself (mem.go:71 keeps the caller's slice): no copy of the chunk bytes.
+  Status PutBlob(const Ref& ref, const Blob& b, bool* added) override;
   // bs.DeleterStore (store.go:50-54): removes ref if present; absent refs are not an error
   // (mem.go:79-85).
   Status Delete(const Ref& ref);
@@ -95,7 +112,7 @@ class MemStore : public Store, public RefPutter {
 
  private:
   mutable std::mutex mu_;
-  std::map<Ref, std::vector<uint8_t>> blobs_;
+  std::map<Ref, Blob> blobs_;
   GpuHasher hasher_;
 };
 
@@ -175,11 +192,18 @@ class Writer {
   bsg_ctx* ctx_ = nullptr;
   // Stream bytes not yet emitted as chunks, kept as the Write() pieces they arrived in: a
   // piece is dropped once every byte of it is in an emitted chunk, so nothing is ever moved.
-  std::deque<std::vector<uint8_t>> pieces_;
+  // Chunks inside one piece are handed to the store as aliases of it (Blob), so the piece
+  // lives on in the store for as long as a chunk of it does.
+  struct Piece {
+    std::shared_ptr<uint8_t> buf;
+    size_t size = 0;
+  };
+  std::deque<Piece> pieces_;
+  Status Copy(const uint8_t* p, size_t n, uint8_t* dst);  // into dst and pinned staging
   uint64_t base_ = 0;          // stream offset of pieces_.front()[0]
   uint64_t end_ = 0;           // stream offset one past the last byte written
   uint64_t emitted_ = 0;       // stream offset of the next chunk to emit
-  std::vector<uint8_t> span_;  // scratch for a chunk that spans pieces
+
   std::vector<std::unique_ptr<TBNode>> levels_;
   std::vector<bsg_chunk> drained_;
   Ref root_{};
