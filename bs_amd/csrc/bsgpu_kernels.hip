@@ -1164,13 +1164,17 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   }
   const uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
 #if BSG_BANK_ROUNDS
-  // skewed lane pairs (2p: E, 2p+1: A); half states A: H0..H3, E: H6, H7, H4, H5
+  // Pair tickets: skewed lane pairs (2p: E, 2p+1: A). Solo and group tickets: skewed octets
+  // (one chain per 8 lanes, E quad at positions 0-3, A quad at 4-7; 8 VALU per round against
+  // the pair's 9). Half states A: H0..H3, E: H6, H7, H4, H5.
   const SkewLane bl = skew_lane();
+  const OctLane ol = oct_lane();
+  const bool a_side = pairs ? bl.a_side : ol.a_side;
   uint32_t hs[4];
-  hs[0] = bl.a_side ? st[0] : st[6];
-  hs[1] = bl.a_side ? st[1] : st[7];
-  hs[2] = bl.a_side ? st[2] : st[4];
-  hs[3] = bl.a_side ? st[3] : st[5];
+  hs[0] = a_side ? st[0] : st[6];
+  hs[1] = a_side ? st[1] : st[7];
+  hs[2] = a_side ? st[2] : st[4];
+  hs[3] = a_side ? st[3] : st[5];
 #endif
   for (uint32_t base = 0; base < nmax; base += B) {
     // phase A: block base + lane % B of chain cA into LDS row `lane`; past a chain's last
@@ -1210,8 +1214,12 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     const uint32_t steps = min(B, nmax - base);
 #if BSG_BANK_ROUNDS
     const uint32_t* ones = ring + 64 * kLongRow;
-    sha256_blocks_skew(hs, bl.a_side ? ones : ring + cR * B * kLongRow,
-                       bl.a_side ? 0u : 4u * kLongRow, steps, (int32_t)nb - (int32_t)base, bl);
+    const uint32_t* krow = a_side ? ones : ring + cR * B * kLongRow;
+    const uint32_t stride = a_side ? 0u : 4u * kLongRow;
+    if (pairs)
+      sha256_blocks_skew(hs, krow, stride, steps, (int32_t)nb - (int32_t)base, bl);
+    else
+      sha256_blocks_oct(hs, krow, stride, steps, (int32_t)nb - (int32_t)base, ol);
 #else
     for (uint32_t i = 0; i < steps; ++i) {
       const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + (cR * B + i) * kLongRow);
@@ -1233,8 +1241,9 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     ring_sync();
   }
 #if BSG_BANK_ROUNDS
-  // each lane collects its chain's first pair: H0..H3 from the A lane, H4..H7 from the E lane
-  const int pe = (int)(lane & ~(B - 1u)), pa = (int)((lane & ~(B - 1u)) | 1u);
+  // each lane collects its chain's state: H0..H3 from an A lane (the pair's odd lane, the
+  // octet's position 4), H4..H7 from its E lane
+  const int pe = (int)(lane & ~(B - 1u)), pa = (int)((lane & ~(B - 1u)) | (pairs ? 1u : 4u));
 #pragma unroll
   for (int k = 0; k < 4; ++k) st[k] = (uint32_t)__shfl((int)hs[k], pa);
   st[6] = (uint32_t)__shfl((int)hs[0], pe);

@@ -329,4 +329,51 @@ __device__ __forceinline__ void sha256_blocks_skew(uint32_t (&hs)[4], const uint
                : "memory", BSG_SKEW_LOOP_CLOBBERS);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skewed octet (wave mode, solo and group tickets): one chain per 8 lanes, E quad at octet
+// positions 0-3, A quad at 4-7, every lane of a quad holding the same values. Same skew and
+// slot convention as the pair; a Sigma is one per-lane-count rotate (quad positions rotate by
+// 6, 11, 25, 6 on E, by 2, 13, 22, 2 on A) and two DPP xors within the quad, and the exchange
+// reads the mirror lane of the half-row (always in the other quad): 8 VALU per round, 64
+// bytes of code, against the pair's 9 and 72 (tools/gen_skew_asm.py, main_loop_oct).
+struct OctLane {
+  uint32_t rot, xm;
+  bool a_side;
+};
+
+__device__ __forceinline__ OctLane oct_lane() {
+  OctLane b;
+  const uint32_t p = threadIdx.x & 7u;
+  b.a_side = p >= 4u;
+  const uint32_t q = p & 3u;
+  // E: 6, 11, 25, 6   A: 2, 13, 22, 2
+  const uint32_t re = q == 1u ? 11u : (q == 2u ? 25u : 6u);
+  const uint32_t ra = q == 1u ? 13u : (q == 2u ? 22u : 2u);
+  b.rot = b.a_side ? ra : re;
+  b.xm = b.a_side ? 0xffffffffu : 0u;
+  return b;
+}
+
+// `nblk` consecutive blocks (wave-uniform) of the skewed octets, block k's K+W row at
+// row + k * stride bytes (A lanes: stride 0 on their row of ones); an octet whose chain has
+// only `lim` blocks left stops after them (exec-masked). hs as for the pair: A lanes
+// (H0,H1,H2,H3), E lanes (H6,H7,H4,H5).
+#include "sha256_oct_loop.inc"
+__device__ __forceinline__ void sha256_blocks_oct(uint32_t (&hs)[4], const uint32_t* row,
+                                                  uint32_t stride, uint32_t nblk, int32_t lim,
+                                                  const OctLane& b) {
+  if (nblk == 0) return;
+  const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const uint32_t*)row);
+  const uint64_t amask = 0xF0F0F0F0F0F0F0F0ull;  // A lanes: octet positions 4-7
+  uint32_t cnt;
+  uint64_t sexec;
+  asm volatile(BSG_OCT_LOOP_ASM
+               : [h0] "+v"(hs[0]), [h1] "+v"(hs[1]), [h2] "+v"(hs[2]), [h3] "+v"(hs[3]),
+                 [cnt] "=&s"(cnt), [sexec] "=&s"(sexec)
+               : [addr] "v"(addr), [stride] "v"(stride), [nblk] "s"(nblk), [lim] "v"(lim),
+                 [xm] "v"(b.xm), [s1] "v"(b.rot), [amask] "s"(amask)
+               : "memory", BSG_OCT_LOOP_CLOBBERS);
+}
+
 }  // namespace bsg
