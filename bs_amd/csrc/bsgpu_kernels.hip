@@ -37,6 +37,13 @@
 #ifndef BSG_PAIR_PCT
 #define BSG_PAIR_PCT 30
 #endif
+// With the octet chains (round 2) a lightly loaded launch — all its blocks are less than a
+// tenth of what the chip's lanes hash while the longest chain runs — ends on the pair tickets
+// unless the group tier reaches further down: configs[1] 88.2 GiB/s at 56 %, 93.1 at 48 %
+// (same chain end), while configs[2] (loaded, per-lane throughput decides) is best at 56 %.
+#ifndef BSG_TLEN_PCT_LIGHT
+#define BSG_TLEN_PCT_LIGHT 48
+#endif
 
 namespace bsg {
 
@@ -1012,7 +1019,8 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   const uint32_t t = threadIdx.x;
   if (t == 0) nok = 0;
   const uint64_t mx = a.ctr->max_nblocks, w = a.ctr->bucket_width;
-  uint64_t tlen = (mx * BSG_TLEN_PCT) / 100;
+  const bool light = a.ctr->total_blocks * 10ull < mx * 64ull * a.waves;
+  uint64_t tlen = (mx * (light ? BSG_TLEN_PCT_LIGHT : BSG_TLEN_PCT)) / 100;
   const uint64_t share = (a.ctr->total_blocks * 9) / (10ull * 64ull * a.waves);
   tlen = max(max(tlen, share), (uint64_t)kLongMinBlocks);
   uint64_t cap = kSolo + (uint64_t)kGroup * (a.waves / 2 > kSolo ? a.waves / 2 - kSolo : 0);
