@@ -11,11 +11,20 @@ __device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_
 __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t r) {
   return __builtin_amdgcn_alignbit(x, x, r);
 }
-// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor.
+// 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor
+// for a ^ b ^ c. BSG_BITOP3_ASM=1 uses inline asm (round 1); by default the compiler builtin,
+// which the scheduler can move like any other instruction.
+#ifndef BSG_BITOP3_ASM
+#define BSG_BITOP3_ASM 0
+#endif
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if BSG_BITOP3_ASM
   uint32_t r;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
+#else
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -34,9 +43,13 @@ static constexpr uint32_t kK256[64] = {
 template <uint32_t TT>
 __device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
   // v_bitop3_b32: bit i of the result = TT[(a_i << 2) | (b_i << 1) | c_i]
+#if BSG_BITOP3_ASM
   uint32_t r;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
   return r;
+#else
+  return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+#endif
 }
 
 // One SHA-256 round, 14 VALU ops: 3+1 (Sigma1), Ch (bitop3 0xCA), h+K+W, add3, d += T1,
