@@ -161,19 +161,24 @@ def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str) -> d
 
 
 def chain_roofline(diag: dict) -> dict | None:
-    """k_sha's real bound: the longest chunk's serial SHA-256 chain. Floor = 66 iterations x 9
-    VALU per 64-round block (sha256_skew_loop.inc) at the SIMD's 4 cycles per wave64 VALU
-    instruction; achieved = the in-kernel s_memtime cycles per block of the longest job."""
+    """k_sha's real bound: the longest chunk's serial SHA-256 chain, run by a skewed octet
+    (sha256_oct_loop.inc: 544 VALU per 64-round block). Two floors: the SIMD's 4 cycles per
+    wave64 VALU instruction, and the instruction-fetch model of DESIGN §4.1 (a lone wave takes
+    in ~1.56 bytes of code per cycle; the loop is 4,308 bytes of VALU code per block). achieved = the
+    in-kernel s_memtime cycles per block of the longest job."""
     try:
         cyc = float(diag["long"]["cycles_per_block"])
     except (KeyError, TypeError, ValueError):
         return None
     if cyc <= 0:
         return None
-    floor = 66 * 9 * 4.0
-    return {"bound": "issue (serial chain)", "kernel": "k_sha wave mode",
-            "floor_cycles_per_block": floor, "achieved_cycles_per_block": round(cyc, 1),
-            "frac": round(floor / cyc, 4), "blocks": diag["long"].get("blocks")}
+    valu = 544
+    floor = valu * 4.0
+    fetch = 4308 / 1.56
+    return {"bound": "issue / instruction fetch (serial chain)", "kernel": "k_sha wave mode",
+            "floor_cycles_per_block": floor, "fetch_model_cycles_per_block": round(fetch, 1),
+            "achieved_cycles_per_block": round(cyc, 1), "frac": round(floor / cyc, 4),
+            "frac_of_fetch_model": round(fetch / cyc, 4), "blocks": diag["long"].get("blocks")}
 
 
 def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:

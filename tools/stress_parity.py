@@ -25,6 +25,9 @@ def main():
         rng = np.random.default_rng(seed_base + d)
         bits = int(rng.integers(10, 23))
         mn = int(rng.choice([64, 512, 1024, 4096]))
+        if rng.random() < 0.1:   # the full ranges split.Bits / split.MinSize accept
+            bits = int(rng.choice([4, 6, 8, 12, 33, 40]))
+            mn = int(rng.choice([1, 17, 63, 64]))
         if d % 2 == 0:  # batch of streams, lengths up to 8 MB
             ns = int(rng.integers(1, 40))
             lens = [int(x) for x in rng.integers(0, 8_000_000, size=ns)]
