@@ -13,3 +13,5 @@ OUT=prof_c1 BENCH_ARGS="--cpu-sample-mib 0 --e2e-mib 0" bash tools/gpu_trace_arg
 OUT=prof_c2 bash tools/gpu_trace_args.sh || exit $?
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch -o run --output-format csv -- ./tools/ubench/scan_calib > $O/calib_fetch.log 2>&1 || exit $?
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d $O/calib_write -o run --output-format csv -- ./tools/ubench/scan_calib > $O/calib_write.log 2>&1
+timeout -k 10 300 python tools/writer_bench.py > $O/writer_bench.log 2>&1 || exit $?
+E2E_TILES=256 timeout -k 10 300 python tools/e2e_bench.py > $O/e2e.log 2>&1
