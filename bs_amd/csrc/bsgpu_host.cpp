@@ -165,7 +165,7 @@ struct bsg_engine {
   int num_cus = 256;
   hipStream_t stream = nullptr;
   DevBuf table, streams, strip0, counts, refine, slots, strip_off, partials_a, partials_b, cand, flags,
-      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets;
+      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets, jinfo;
   PinBuf h_streams, h_strip0, h_ctr;
   // Optional snapshot right after selection (streaming pipeline): the counters and every
   // stream's last chunk end land in pinned memory and sel_ev fires, long before k_sha ends.
@@ -237,6 +237,7 @@ struct bsg_engine {
     HCHECK(ctr.ensure(sizeof(Counters)));
     HCHECK(long_list.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(order.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
+    HCHECK(jinfo.ensure(sizeof(uint32_t) * (chunk_cap + ns)));
     HCHECK(buckets.ensure(sizeof(uint32_t) * 4 * kLptBuckets));
     HCHECK(h_streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(h_strip0.ensure(sizeof(uint64_t) * (ns + 1)));
@@ -325,7 +326,7 @@ struct bsg_engine {
                carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
                buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
                buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
-               long_mode(), 4u * (uint32_t)num_cus};
+               jinfo.as<uint32_t>(), long_mode(), 4u * (uint32_t)num_cus};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
@@ -854,7 +855,7 @@ void bsg_engine_destroy(bsg_engine* e) {
   DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->refine, &e->slots,
                     &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
                     &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
-                    &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets};
+                    &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets, &e->jinfo};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 4; ++i)
     if (e->ev[i]) hipEventDestroy(e->ev[i]);

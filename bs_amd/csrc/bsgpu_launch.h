@@ -83,6 +83,8 @@ struct ShaArgs {
   uint32_t* bucket_elig;    // [kLptBuckets] wave-eligible jobs per bucket, zeroed per run
   uint32_t* bucket_off;     // [kLptBuckets] per-lane order offsets
   uint32_t* bucket_loff;    // [kLptBuckets] long-list offsets
+  uint32_t* jinfo;          // [chunk_cap + nstreams] per job, from k_lens: nblocks | eligible
+                            // << 31, or kNoJob (no job: a short open chunk carried as bytes)
   int long_mode;            // 0 auto, 1 per-lane only, 2 wave mode only (experiments)
   uint32_t waves;           // waves of the k_sha grid (4 per CU)
 };
