@@ -194,7 +194,9 @@ __device__ __forceinline__ bool chain64(const uint32_t* tab, const uint32_t (&wn
                                         uint32_t (&hin)[64], const uint32_t (&hcur)[64],
                                         uint32_t& h, uint32_t lane4, uint32_t mask) {
   if (WIDE) {
-    u16x2 m = u16x2{0xffff, 0xffff};
+    // min of the low 16 bits of the running min and both hashes in one v_min3_u16 (round 1:
+    // a v_perm packing two hashes + a v_pk_min_u16, one VALU per byte instead of a half)
+    uint32_t m = 0xffffu;
 #pragma unroll
     for (int k = 0; k < 64; k += 2) {
       const uint32_t h0 = xor3(rotl1(h), hin[k], hcur[k]);
@@ -203,10 +205,9 @@ __device__ __forceinline__ bool chain64(const uint32_t* tab, const uint32_t (&wn
         hin[k] = lds_at(tab, tab_addr(wnext[k >> 2], lane4, k));
         hin[k + 1] = lds_at(tab, tab_addr(wnext[(k + 1) >> 2], lane4, k + 1));
       }
-      const uint32_t pk = __builtin_amdgcn_perm(h, h0, 0x05040100u);  // lo16(h0) | lo16(h)<<16
-      m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, pk));
+      asm("v_min3_u16 %0, %1, %2, %3" : "=v"(m) : "v"(m), "v"(h0), "v"(h));
     }
-    return m.x == 0 || m.y == 0;
+    return (m & 0xffffu) == 0;
   } else {
     uint32_t m = 0xffffffffu;
 #pragma unroll
@@ -606,9 +607,12 @@ __global__ __launch_bounds__(kScanT) void k_prefix_down(PrefixArgs a) {
   uint64_t pre = a.partials[blockIdx.x];
   for (uint32_t wv = 0; wv < (threadIdx.x >> 6); ++wv) pre += wsum[wv];
   pre += x - s;
+  // Offsets are only read where the input is non-zero (k_compact / k_rescan for strips with
+  // candidates, k_chunks for flagged candidates), so only those are written: on configs[2]
+  // this is ~250 K of 8 M strip offsets.
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
-    if (first + i < n) a.out[first + i] = pre;
+    if (first + i < n && v[i]) a.out[first + i] = pre;
     pre += v[i];
   }
 }
