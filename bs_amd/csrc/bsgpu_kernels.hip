@@ -44,6 +44,9 @@
 #ifndef BSG_TLEN_PCT_LIGHT
 #define BSG_TLEN_PCT_LIGHT 48
 #endif
+#ifndef BSG_PAIR_PCT_LIGHT
+#define BSG_PAIR_PCT_LIGHT 30
+#endif
 
 namespace bsg {
 
@@ -1086,10 +1089,11 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   const uint32_t n8 = block_scan4(lv, lo, wsum);
   const uint64_t t8 = n8 <= kSolo ? n8 : kSolo + (n8 - kSolo + kGroup - 1) / kGroup;
   uint32_t nlb = nlb8;
-  if (BSG_PAIR_PCT > 0 && a.long_mode == 0) {
-    // the next buckets, down to BSG_PAIR_PCT % of the longest, on pair tickets within the
+  const uint64_t pair_pct = light ? BSG_PAIR_PCT_LIGHT : BSG_PAIR_PCT;
+  if (pair_pct > 0 && a.long_mode == 0) {
+    // the next buckets, down to pair_pct % of the longest, on pair tickets within the
     // remaining half-of-the-waves ticket budget
-    const uint64_t tlen2 = max((mx * BSG_PAIR_PCT) / 100, (uint64_t)kLongMinBlocks);
+    const uint64_t tlen2 = max((mx * pair_pct) / 100, (uint64_t)kLongMinBlocks);
     const uint64_t tb = a.waves / 2 > t8 ? a.waves / 2 - t8 : 0;
     const uint64_t cap2 = tb * kPairGroup;
     uint32_t ok2 = 0;

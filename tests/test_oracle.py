@@ -159,3 +159,19 @@ def test_edit_stream_boundaries_resynchronise(oracle, table):
     refs_a = {bytes(r) for r in ca["ref"]}
     shared = sum(bytes(r) in refs_a for r in cb["ref"]) / len(cb)
     assert 0.75 < shared < 1.0, shared
+
+
+def test_sha256_implementations_agree(oracle):
+    """The C oracle's SHA-256 with the x86 SHA extensions (the CPU baseline's, as Go's amd64
+    crypto/sha256) and its scalar FIPS 180-4 compression give hashlib's digests."""
+    rng = np.random.default_rng(5)
+    msgs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            for n in list(range(0, 300)) + [1000, 4096, 100_000]]
+    try:
+        for ni in (True, False):
+            impl = oracle.sha256_use(ni)
+            assert impl == ("scalar" if not ni else impl)
+            for m in msgs:
+                assert oracle.sha256(m) == hashlib.sha256(m).digest(), (impl, len(m))
+    finally:
+        oracle.sha256_use(True)
