@@ -660,7 +660,12 @@ struct bsg_ctx {
 
   // Host side of Write: bytes into the current slot's pinned staging (large pieces on several
   // threads), submitting full tiles as more data arrives.
+  // Stream offsets travel in 40-bit candidate fields (bsgpu_internal.h): 1 TiB per stream.
+  static constexpr uint64_t kMaxStream = 1ull << 40;
+  bool too_long(size_t n) const { return pos + fill + n >= kMaxStream; }
+
   int write(const uint8_t* p, size_t n) {
+    if (too_long(n)) return BSG_EINVAL;
     while (n) {
       if (fill == tile) {  // full tile and more data coming: submit it (never the last one)
         int rc = submit(false);
@@ -715,7 +720,7 @@ struct bsg_ctx {
     return BSG_OK;
   }
   int commit(size_t n) {
-    if (n > std::min(slots[cur].staging.cap, tile) - fill) return BSG_EINVAL;
+    if (n > std::min(slots[cur].staging.cap, tile) - fill || too_long(n)) return BSG_EINVAL;
     fill += n;
     return poll();
   }

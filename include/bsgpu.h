@@ -78,7 +78,8 @@ typedef struct bsg_ctx bsg_ctx;
 bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table /* 256 or NULL */,
                   int* err);
 /* Copies p[0..n) into pinned staging (the caller keeps ownership of p); full tiles are split
- * and hashed on the device as they fill. */
+ * and hashed on the device as they fill. A stream may hold up to 2^40 - 1 bytes (1 TiB; stream
+ * offsets travel in 40-bit fields on the device): a Write past that returns BSG_EINVAL. */
 int bsg_write(bsg_ctx* ctx, const uint8_t* p, size_t n);
 /* Zero-copy Write: *p / *cap = the free rest of the current pinned staging buffer (never more
  * than the rest of the tile; the buffer grows from 4 MiB to the tile size as the stream does,
@@ -110,7 +111,8 @@ typedef struct bsg_engine bsg_engine;
 bsg_engine* bsg_engine_create(int device, const uint32_t* table /* 256 or NULL */, int* err);
 void bsg_engine_destroy(bsg_engine* eng);
 /* Enqueue split + hash of nstreams streams d_data[off[i] .. off[i]+len[i]) (device memory,
- * off[i] % 16 == 0; off/len are host arrays). Asynchronous on the engine's stream.
+ * off[i] % 16 == 0; off/len are host arrays; at most 65,535 streams of < 2^40 bytes each).
+ * Asynchronous on the engine's stream.
  * The allocation holding d_data must extend at least BSG_READ_SLACK bytes past the end of the
  * last stream (the SHA-256 loader reads whole 64-byte blocks and masks the excess). */
 #define BSG_READ_SLACK 256
