@@ -155,9 +155,29 @@ def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str) -> d
                                 threads=threads)
         dt = time.perf_counter() - t0
         nch = len(ch)
+    full = cpu_full_writer(O, table, host_streams, bits, min_size, threads)
     return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{sample} (same bytes/params), C oracle split + sha256 ({impl}), "
-                      f"{threads} thread(s), one stream per thread, {nch} chunks in {dt:.2f}s"}
+                      f"{threads} thread(s), one stream per thread, {nch} chunks in {dt:.2f}s",
+            "full_writer": full}
+
+
+def cpu_full_writer(O, table, host_streams: list, bits: int, min_size: int, threads: int) -> dict:
+    """SURVEY §8(d)'s "full" CPU variant: split.Writer end to end (oracle bso_writer_root:
+    Splitter + sha256 + TreeBuilder + PutProto of every node, each blob copied as store/mem's
+    Put keeps Go's appended chunk) over the same sample, one stream per thread (ctypes drops the
+    GIL, so the threads run the C code in parallel)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = sum(len(a) for a in host_streams)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        res = list(ex.map(lambda a: O.writer_root(table, a, bits=bits, min_size=min_size,
+                                                  fanout=8, keep_copies=True), host_streams))
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "puts": sum(p for _, p in res),
+            "sample": f"same sample, split.Writer -> store/mem restated in C, Fanout 8, "
+                      f"{dt:.2f}s"}
 
 
 def chain_roofline(diag: dict) -> dict | None:

@@ -477,3 +477,193 @@ size_t bso_split_streams(const uint32_t table[256], const uint8_t* base, const u
     pthread_mutex_destroy(&j.mu);
     return total;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * split.Writer end to end (CPU restatement, test infrastructure and the "full Writer" CPU
+ * baseline): the Splitter above, then hashsplit's TreeBuilder as wired by split.NewWriter
+ * (split/split.go:51-90: Add(chunk, level / fanout); F PutProto's child nodes and Put's chunks
+ * into Node{Offset, Size, Nodes, Leaves}), Writer.Close (split.go:104-126: TreeBuilder.Root,
+ * PutProto(root)). The TreeBuilder rules are restated as in oracle.py's py_tree_root (recalled,
+ * Go-unpinned: DESIGN.md §2). store/mem Puts are emulated by copying each blob (Go's Splitter
+ * builds every chunk by appending its bytes; mem.go:71 keeps that slice).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct wnode wnode;
+typedef struct { uint8_t ref[32]; uint64_t off; wnode* node; } wchild; /* node: child Node */
+struct wnode { wchild* nodes; size_t nn; wchild* leaves; size_t nl; uint64_t offset, size; };
+typedef struct { wnode** nodes; size_t nn, cn; wchild* chunks; size_t nc, cc;
+                 uint64_t offset, size; } tbnode;
+typedef struct {
+    tbnode* lv; size_t nlv, clv;
+    wnode** all; size_t nall, call;        /* every wnode made, freed at the end */
+    uint8_t** blobs; size_t nblobs, cblobs; /* emulated store/mem copies */
+    int keep;
+    unsigned fanout;
+} wstate;
+
+static void* grow(void* p, size_t* cap, size_t need, size_t elt) {
+    if (need <= *cap) return p;
+    size_t nc = *cap ? *cap * 2 : 8;
+    while (nc < need) nc *= 2;
+    *cap = nc;
+    return realloc(p, nc * elt);
+}
+
+static void ws_put(wstate* w, const uint8_t* b, size_t n, uint8_t ref[32]) {
+    bso_sha256(b, n, ref);
+    if (!w->keep) return;
+    w->blobs = (uint8_t**)grow(w->blobs, &w->cblobs, w->nblobs + 1, sizeof(uint8_t*));
+    uint8_t* c = (uint8_t*)malloc(n ? n : 1);
+    memcpy(c, b, n);
+    w->blobs[w->nblobs++] = c;
+}
+
+static size_t put_varint(uint8_t* o, uint64_t v) {
+    size_t k = 0;
+    while (v >= 0x80) { o[k++] = (uint8_t)(v | 0x80); v >>= 7; }
+    o[k++] = (uint8_t)v;
+    return k;
+}
+
+/* split.proto Node, deterministic proto3 as Go's proto.Marshal (fields in order, zeros
+ * omitted); returns the length written into o (o must hold 50 * (nn + nl) + 24 bytes). */
+static size_t marshal_node(const wnode* n, uint8_t* o) {
+    size_t k = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const wchild* cs = pass ? n->leaves : n->nodes;
+        size_t cnt = pass ? n->nl : n->nn;
+        for (size_t i = 0; i < cnt; i++) {
+            uint8_t c[48];
+            size_t m = 0;
+            c[m++] = 0x0a; c[m++] = 32;
+            memcpy(c + m, cs[i].ref, 32); m += 32;
+            if (cs[i].off) { c[m++] = 0x10; m += put_varint(c + m, cs[i].off); }
+            o[k++] = pass ? 0x12 : 0x0a;
+            k += put_varint(o + k, m);
+            memcpy(o + k, c, m); k += m;
+        }
+    }
+    if (n->offset) { o[k++] = 0x18; k += put_varint(o + k, n->offset); }
+    if (n->size) { o[k++] = 0x20; k += put_varint(o + k, n->size); }
+    return k;
+}
+
+static void put_node(wstate* w, const wnode* n, uint8_t ref[32]) {
+    uint8_t* buf = (uint8_t*)malloc(50 * (n->nn + n->nl) + 24);
+    size_t len = marshal_node(n, buf);
+    ws_put(w, buf, len, ref);
+    free(buf);
+}
+
+static wnode* tb_F(wstate* w, tbnode* t) { /* split/split.go:52-81 */
+    wnode* n = (wnode*)calloc(1, sizeof(wnode));
+    w->all = (wnode**)grow(w->all, &w->call, w->nall + 1, sizeof(wnode*));
+    w->all[w->nall++] = n;
+    n->offset = t->offset;
+    n->size = t->size;
+    uint64_t off = t->offset;
+    n->nodes = (wchild*)malloc((t->nn ? t->nn : 1) * sizeof(wchild));
+    for (size_t i = 0; i < t->nn; i++) {
+        put_node(w, t->nodes[i], n->nodes[i].ref);  /* bs.PutProto(child) */
+        n->nodes[i].off = off;
+        n->nodes[i].node = t->nodes[i];
+        off += t->nodes[i]->size;
+    }
+    n->nn = t->nn;
+    n->leaves = (wchild*)malloc((t->nc ? t->nc : 1) * sizeof(wchild));
+    for (size_t i = 0; i < t->nc; i++) {  /* chunks were Put when added: refs in chunks[] */
+        memcpy(n->leaves[i].ref, t->chunks[i].ref, 32);
+        n->leaves[i].off = off;
+        n->leaves[i].node = NULL;
+        off += t->chunks[i].off;  /* chunks[].off holds the chunk length */
+    }
+    n->nl = t->nc;
+    return n;
+}
+
+static void tb_reset(tbnode* t, uint64_t offset) {
+    t->nn = 0; t->nc = 0; t->offset = offset; t->size = 0;
+}
+
+static void tb_add(wstate* w, const uint8_t ref[32], uint64_t len, unsigned level) {
+    if (w->nlv == 0) {
+        w->lv = (tbnode*)grow(w->lv, &w->clv, 1, sizeof(tbnode));
+        memset(&w->lv[0], 0, sizeof(tbnode));
+        w->nlv = 1;
+    }
+    tbnode* l0 = &w->lv[0];
+    l0->chunks = (wchild*)grow(l0->chunks, &l0->cc, l0->nc + 1, sizeof(wchild));
+    memcpy(l0->chunks[l0->nc].ref, ref, 32);
+    l0->chunks[l0->nc].off = len;
+    l0->nc++;
+    for (size_t i = 0; i < w->nlv; i++) w->lv[i].size += len;
+    for (unsigned i = 0; i < level; i++) {
+        if (i == w->nlv - 1) {
+            w->lv = (tbnode*)grow(w->lv, &w->clv, w->nlv + 1, sizeof(tbnode));
+            memset(&w->lv[w->nlv], 0, sizeof(tbnode));
+            w->lv[w->nlv].offset = w->lv[i].offset;
+            w->lv[w->nlv].size = w->lv[i].size;
+            w->nlv++;
+        }
+        wnode* f = tb_F(w, &w->lv[i]);
+        tbnode* up = &w->lv[i + 1];
+        up->nodes = (wnode**)grow(up->nodes, &up->cn, up->nn + 1, sizeof(wnode*));
+        up->nodes[up->nn++] = f;
+        tb_reset(&w->lv[i], up->offset + up->size);
+    }
+}
+
+size_t bso_writer_root(const uint32_t table[256], const uint8_t* x, size_t n, unsigned split_bits,
+                       unsigned min_size, unsigned fanout, int keep_copies, uint8_t root[32]) {
+    wstate w;
+    memset(&w, 0, sizeof w);
+    w.keep = keep_copies;
+    w.fanout = fanout ? fanout : 1;
+    memset(root, 0, 32);                      /* no input: Root stays bs.Zero */
+    const size_t ms = min_size ? min_size : 64;
+    const size_t bound = n / ms + 1;
+    bso_chunk* ch = (bso_chunk*)malloc(bound * sizeof(bso_chunk));
+    size_t nch = split_one(table, x, n, split_bits, min_size, 1, ch, bound, 0);
+    for (size_t i = 0; i < nch; i++) {
+        if (keep_copies) {                    /* store/mem Put of the chunk (ref known) */
+            w.blobs = (uint8_t**)grow(w.blobs, &w.cblobs, w.nblobs + 1, sizeof(uint8_t*));
+            uint8_t* c = (uint8_t*)malloc(ch[i].len ? ch[i].len : 1);
+            memcpy(c, x + ch[i].offset, ch[i].len);
+            w.blobs[w.nblobs++] = c;
+        }
+        tb_add(&w, ch[i].ref, ch[i].len, ch[i].level / w.fanout);  /* split/split.go:86 */
+    }
+    free(ch);
+    size_t puts = w.nblobs;
+    if (w.nlv) {
+        /* TreeBuilder.Root: fold every non-empty level below the top into its parent */
+        for (size_t i = 0; i + 1 < w.nlv; i++) {
+            tbnode* t = &w.lv[i];
+            if (!t->nc && !t->nn) continue;
+            wnode* f = tb_F(&w, t);
+            tbnode* up = &w.lv[i + 1];
+            up->nodes = (wnode**)grow(up->nodes, &up->cn, up->nn + 1, sizeof(wnode*));
+            up->nodes[up->nn++] = f;
+        }
+        wnode* r;
+        if (w.nlv == 1) {
+            r = tb_F(&w, &w.lv[0]);
+        } else {
+            tbnode* top = &w.lv[w.nlv - 1];
+            if (top->nn > 1) {
+                r = tb_F(&w, top);
+            } else {                          /* prune single-child roots (their F already ran) */
+                r = top->nodes[0];
+                while (r->nn == 1) r = r->nodes[0].node;
+            }
+        }
+        put_node(&w, r, root);                /* PutProto(root) -> Writer.Root */
+        puts = w.nblobs;
+    }
+    for (size_t i = 0; i < w.nlv; i++) { free(w.lv[i].nodes); free(w.lv[i].chunks); }
+    free(w.lv);
+    for (size_t i = 0; i < w.nall; i++) { free(w.all[i]->nodes); free(w.all[i]->leaves); free(w.all[i]); }
+    free(w.all);
+    for (size_t i = 0; i < w.nblobs; i++) free(w.blobs[i]);
+    free(w.blobs);
+    return puts;
+}

@@ -65,6 +65,14 @@ size_t bso_split_streams(const uint32_t table[256], const uint8_t* base, const u
                          unsigned min_size, int threads, bso_chunk* out, size_t cap,
                          uint64_t* counts);
 
+/* split.Writer end to end: Splitter, TreeBuilder (level / fanout), F, PutProto, Close ->
+ * root = Writer.Root (bs.Zero for no input). keep_copies != 0 also copies every blob as a
+ * store/mem Put of Go's appended chunk would (the "full Writer" CPU baseline); returns the
+ * number of blobs put (with keep_copies) or 0. The TreeBuilder rules are recalled
+ * (Go-unpinned), the same as oracle.py's py_tree_root. */
+size_t bso_writer_root(const uint32_t table[256], const uint8_t* x, size_t n, unsigned split_bits,
+                       unsigned min_size, unsigned fanout, int keep_copies, uint8_t root[32]);
+
 #ifdef __cplusplus
 }
 #endif

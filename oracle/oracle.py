@@ -72,6 +72,9 @@ def lib():
         L.bso_split_streams.argtypes = [u32p, u8p, u64p, u64p, ctypes.c_uint32, ctypes.c_uint,
                                         ctypes.c_uint, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_size_t, u64p]
+        L.bso_writer_root.restype = ctypes.c_size_t
+        L.bso_writer_root.argtypes = [u32p, u8p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint,
+                                      ctypes.c_uint, ctypes.c_int, u8p]
         _lib = L
     return _lib
 
@@ -153,6 +156,19 @@ def split_streams(table: np.ndarray, base: np.ndarray, off, lens, bits: int = 16
                                 _p(counts, ctypes.c_uint64))
     assert n <= cap
     return out[:n], counts
+
+
+def writer_root(table: np.ndarray, data, bits: int = 16, min_size: int = 1024, fanout: int = 8,
+                keep_copies: bool = False) -> tuple[bytes, int]:
+    """split.Writer end to end in C (Splitter + TreeBuilder + PutProto + Close): (Root, puts).
+    keep_copies also copies every blob as store/mem's Put would (puts counts them)."""
+    x = data if isinstance(data, np.ndarray) else np.frombuffer(bytes(data), dtype=np.uint8)
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    t = np.ascontiguousarray(table, dtype=np.uint32)
+    root = np.zeros(32, dtype=np.uint8)
+    puts = lib().bso_writer_root(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits,
+                                 min_size, fanout, int(keep_copies), _p(root, ctypes.c_uint8))
+    return root.tobytes(), int(puts)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -188,3 +188,16 @@ def test_gc_config1_commonsense(gpu, oracle, table):
     assert chunk_refs <= set(st.refs())
     assert root in set(st.refs())
     assert gpu.Reader(st, root).read_all() == data
+
+
+@pytest.mark.parametrize("bits,min_size,fanout", [(16, 1024, 8), (13, 64, 4), (10, 64, 2)])
+def test_writer_root_256mib_matches_c_writer(gpu, oracle, table, bits, min_size, fanout):
+    """Writer.Root over 256 MiB (32 MiB writes, several pipeline windows) == the C restatement
+    of split.Writer (oracle bso_writer_root: Splitter + TreeBuilder + PutProto)."""
+    from bs_amd.synth import splitmix_array
+    data = splitmix_array(0x5EED0256, 256 << 20)
+    st, root = write_all(gpu, memoryview(data), piece=32 << 20, bits=bits, min_size=min_size,
+                         fanout=fanout)
+    want, _ = oracle.writer_root(table, data, bits=bits, min_size=min_size, fanout=fanout)
+    assert root == want
+    st.free()

@@ -175,3 +175,33 @@ def test_sha256_implementations_agree(oracle):
                 assert oracle.sha256(m) == hashlib.sha256(m).digest(), (impl, len(m))
     finally:
         oracle.sha256_use(True)
+
+
+@pytest.mark.parametrize("name,bits,min_size,fanout", [
+    ("commonsense.txt", 16, 1024, 8), ("commonsense.txt", 8, 64, 2), ("commonsense.txt", 4, 0, 1),
+    ("yubnub.opus", 4, 1024, 2), ("yubnub.opus", 12, 1024, 4), ("yubnub.opus", 16, 1024, 8)])
+def test_c_writer_root_matches_python_tree(oracle, table, name, bits, min_size, fanout):
+    """bso_writer_root (C, the full-Writer CPU baseline) == py_tree_root over the same chunks."""
+    data = read_golden(name)
+    ch = oracle.split(table, data, bits=bits, min_size=min_size)
+    store = {}
+    want = oracle.py_tree_root(
+        [(data[int(c["offset"]):int(c["offset"] + c["len"])], int(c["level"])) for c in ch],
+        fanout, store)
+    root, puts = oracle.writer_root(table, data, bits=bits, min_size=min_size, fanout=fanout,
+                                    keep_copies=True)
+    assert root == want
+    assert puts >= len(store)  # every chunk and node Put (duplicates included)
+    assert oracle.writer_root(table, data, bits=bits, min_size=min_size, fanout=fanout)[0] == want
+
+
+def test_c_writer_root_empty_and_synthetic(oracle, table):
+    assert oracle.writer_root(table, b"")[0] == bytes(32)  # Root stays bs.Zero
+    from bs_amd.synth import splitmix_bytes
+    data = splitmix_bytes(7, 3_000_000)
+    for bits, fanout in ((10, 2), (13, 8), (16, 4)):
+        ch = oracle.split(table, data, bits=bits, min_size=64)
+        want = oracle.py_tree_root(
+            [(data[int(c["offset"]):int(c["offset"] + c["len"])], int(c["level"])) for c in ch],
+            fanout)
+        assert oracle.writer_root(table, data, bits=bits, min_size=64, fanout=fanout)[0] == want
