@@ -323,6 +323,8 @@ class Engine:
             out["timeline_us"] = {"long_start": round(float(t[1] - t[0]) * 0.01, 1),
                                   "long_end": round(float(t[2] - t[0]) * 0.01, 1),
                                   "lane_end": round(float(t[3] - t[0]) * 0.01, 1)}
+        if os.environ.get("BSG_DIAG_RAW") == "1":  # experiment builds (BSG_LANE_DIAG)
+            out["diag2_raw"] = [int(x) for x in d[8:13]]
         for tag, o in (("long", 3), ("lane", 8)):
             cyc, rt, nb = int(d[o + 1] - d[o]), int(d[o + 3] - d[o + 2]), int(d[o + 4])
             if nb and rt:

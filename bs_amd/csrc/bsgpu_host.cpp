@@ -165,7 +165,8 @@ struct bsg_engine {
   int num_cus = 256;
   hipStream_t stream = nullptr;
   DevBuf table, streams, strip0, counts, refine, slots, strip_off, partials_a, partials_b, cand, flags,
-      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets, jinfo;
+      fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets, jinfo, jdesc,
+      regions, oreg, rorder;
   PinBuf h_streams, h_strip0, h_ctr;
   // Optional snapshot right after selection (streaming pipeline): the counters and every
   // stream's last chunk end land in pinned memory and sel_ev fires, long before k_sha ends.
@@ -177,6 +178,7 @@ struct bsg_engine {
   std::vector<StreamDesc> descs;
   Params p{};
   uint64_t nstrips = 0, cand_cap = 0, chunk_cap = 0;
+  uint64_t data_span = 1;  // bytes from d_data to the end of the last stream (k_sha regions)
   uint64_t retry_cap = 0;  // exact candidate capacity after an overflow (one re-run)
   uint32_t nstreams = 0;
   bool enqueued = false;
@@ -197,11 +199,13 @@ struct bsg_engine {
     // strips
     std::vector<uint64_t> s0(ns + 1);
     uint64_t strips = 0, total_len = 0, chunk_bound = 0;
+    data_span = 1;
     for (uint32_t s = 0; s < ns; ++s) {
       descs[s].strip0 = strips;
       s0[s] = strips;
       strips += (descs[s].len + kStrip - 1) / kStrip;
       total_len += descs[s].len;
+      data_span = std::max<uint64_t>(data_span, descs[s].data_off + descs[s].len);
       chunk_bound += (descs[s].len + (descs[s].seg_base - descs[s].open_start)) / p.min_size + 2;
     }
     s0[ns] = strips;
@@ -238,6 +242,10 @@ struct bsg_engine {
     HCHECK(long_list.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(order.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(jinfo.ensure(sizeof(uint32_t) * (chunk_cap + ns)));
+    HCHECK(jdesc.ensure(sizeof(LaneJob) * (chunk_cap + ns)));
+    HCHECK(regions.ensure(sizeof(Regions)));
+    HCHECK(oreg.ensure(chunk_cap + ns));
+    HCHECK(rorder.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(buckets.ensure(sizeof(uint32_t) * 4 * kLptBuckets));
     HCHECK(h_streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(h_strip0.ensure(sizeof(uint64_t) * (ns + 1)));
@@ -326,7 +334,8 @@ struct bsg_engine {
                carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
                buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
                buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
-               jinfo.as<uint32_t>(), long_mode(), 4u * (uint32_t)num_cus};
+               jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
+               rorder.as<uint64_t>(), data_span, long_mode(), 4u * (uint32_t)num_cus};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
@@ -860,7 +869,8 @@ void bsg_engine_destroy(bsg_engine* e) {
   DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->refine, &e->slots,
                     &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
                     &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
-                    &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets, &e->jinfo};
+                    &e->out, &e->carry, &e->ctr, &e->long_list, &e->order, &e->buckets, &e->jinfo, &e->jdesc,
+                    &e->regions, &e->oreg, &e->rorder};
   for (DevBuf* b : bufs) b->release();
   for (int i = 0; i < 4; ++i)
     if (e->ev[i]) hipEventDestroy(e->ev[i]);
@@ -978,6 +988,16 @@ int bsg_engine_diag(const bsg_engine* e, uint64_t out[16]) {
   out[14] = e->last.ntickets;
   out[15] = e->last.total_blocks;
   return BSG_OK;
+}
+
+// Experiment tooling (not in include/bsgpu.h): copies the region queues' state, including the
+// per-wave records of BSG_LANE_DIAG builds, after the last run.
+extern "C" int bsg_engine_regions_debug(bsg_engine* e, void* out, uint64_t nbytes) {
+  if (!e || !out || !e->regions.p) return BSG_EINVAL;
+  if (e->setdev()) return BSG_EDEVICE;
+  const uint64_t n = std::min<uint64_t>(nbytes, sizeof(Regions));
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return BSG_EDEVICE;
+  return hipMemcpy(out, e->regions.p, n, hipMemcpyDeviceToHost) == hipSuccess ? BSG_OK : BSG_EDEVICE;
 }
 
 int bsg_engine_timeline(const bsg_engine* e, uint64_t out[4]) {

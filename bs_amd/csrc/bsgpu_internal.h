@@ -113,6 +113,41 @@ struct Counters {
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 
+// Per-lane job descriptor (k_lens writes one per job): per-lane mode prefetches it a few blocks
+// before its current job ends, so starting the next job costs no dependent loads.
+struct LaneJob {
+  uint64_t dptr;               // first data byte of the message (device address)
+  uint64_t start;              // stream offset of the chunk (record offset)
+  uint64_t len;                // message bytes = chunk length (fast jobs)
+  uint32_t stream;
+  uint32_t meta;               // level | kLaneJobSlow
+};
+static_assert(sizeof(LaneJob) == 32, "LaneJob layout");
+constexpr uint32_t kLaneJobSlow = 0x80000000u;  // continued or open chunk: full sha_setup path
+
+// Per-lane job queues by address region (k_sha per-lane mode). A lane's loads go to its own
+// chunk, so the 64 lanes of a wave touch 64 places in HBM per load. With a CU's lanes spread
+// over 16 GiB, 97 % of those loads miss the CU's address-translation cache (UTCL1) and a block
+// costs ~60 % more than with the CU's lanes inside 2 GiB (tools/ubench/lanes_mem.hip,
+// profiles/r02_lanes_tlb.log). The per-lane jobs are therefore regrouped, longest first within
+// each region, into regions of at most kRegionBytes of address span, and all waves of a k_sha
+// workgroup (one per CU) take their jobs from the same region until it runs dry.
+constexpr uint32_t kMaxRegions = 256;
+constexpr uint32_t kRegionSegs = 256;        // segments of the LPT order counted separately
+constexpr uint32_t kMinRegionJobs = 4096;    // fewer per-lane jobs per region: fewer regions
+constexpr uint64_t kRegionBytes = 1ull << 30;
+struct Regions {
+  uint64_t nregions;                         // R (k_bucket_scan), 1 .. kMaxRegions
+  uint64_t rr;                               // round-robin start region of entering waves
+  uint64_t pad_[6];
+  uint64_t head[kMaxRegions];                // pop counters (zeroed by k_rtotal)
+  uint64_t off[kMaxRegions + 1];             // region r's jobs: rorder[off[r] .. off[r + 1])
+  uint64_t pad2_[7];
+  uint32_t cnt[kRegionSegs * kMaxRegions];   // per segment and region: count, then offset
+  uint64_t wdbg[1024 * 4];                   // BSG_LANE_DIAG builds: per k_sha wave, per-lane
+                                             // mode entry / exit time, region moves, iterations
+};
+
 constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave path below 64 KiB
 constexpr uint32_t kSolo = 8;    // wave mode: the kSolo longest jobs run one per wave,
 constexpr uint32_t kGroup = 8;   // the next ones kGroup per wave (one banked lane pair each)

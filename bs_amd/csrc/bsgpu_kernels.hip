@@ -721,6 +721,10 @@ __global__ void k_init(InitArgs a) {
 // jobs from a device queue as they finish, so a wave stays full whatever the length mix.
 // Jobs [0, M) are finished chunks; jobs [M, M + nstreams) are the open chunks of non-final
 // segments (hash whole blocks only, export the midstate).
+// Job info from k_lens (jinfo): nblocks | eligible << 31; kNoJob for ids without a job.
+constexpr uint32_t kNoJob = 0xffffffffu;
+constexpr uint32_t kJobElig = 0x80000000u;
+
 struct ShaJob {
   uint64_t id;          // job index
   uint64_t start, end;  // stream offsets [start, end)
@@ -884,8 +888,325 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
   }
 }
 
-// Per-lane mode: each lane hashes one chunk at a time, pulling jobs from the longest-first
-// order as it finishes (dynamic per-lane queue).
+#ifndef BSG_LANE_DIAG
+#define BSG_LANE_DIAG 0
+#endif
+#ifndef BSG_LANE_PIPE
+#define BSG_LANE_PIPE 1
+#endif
+#ifndef BSG_LANE_LEAD
+#define BSG_LANE_LEAD 4
+#endif
+
+#if BSG_LANE_DIAG
+// experiment: diag2[] = sums over waves of (0), lane-mode cycles, iterations, active
+// lane-iterations, waves (replaces the per-lane job timing)
+#define LANE_DIAG_INIT                                                                      \
+  uint64_t d_it = 0, d_act = 0, d_moves = 0;                                                 \
+  const uint64_t d_t0 = __builtin_amdgcn_s_memtime();                                        \
+  const uint64_t d_rt0 = __builtin_amdgcn_s_memrealtime();
+#define LANE_DIAG_ITER(active) \
+  d_it += 1;                   \
+  d_act += (uint64_t)__popcll(__ballot(active));
+#define LANE_DIAG_END                                                                       \
+  {                                                                                          \
+    const uint64_t d_tot = __builtin_amdgcn_s_memtime() - d_t0;                              \
+    const uint32_t wid = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);                \
+    if ((threadIdx.x & 63u) == 0 && wid < 1024) {                                            \
+      a.reg->wdbg[4 * wid + 0] = d_rt0;                                                      \
+      a.reg->wdbg[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();                           \
+      a.reg->wdbg[4 * wid + 2] = d_moves;                                                    \
+      a.reg->wdbg[4 * wid + 3] = d_it;                                                       \
+    }                                                                                        \
+    uint64_t m_it = d_it, m_act = d_act;                                                     \
+    for (int o = 32; o > 0; o >>= 1) {                                                       \
+      m_it = max(m_it, (uint64_t)__shfl_xor((long long)m_it, o));                            \
+      m_act = max(m_act, (uint64_t)__shfl_xor((long long)m_act, o));                         \
+    }                                                                                        \
+    if ((threadIdx.x & 63u) == 0) {                                                          \
+      auto* d2 = reinterpret_cast<unsigned long long*>(a.ctr->diag2);                        \
+      atomicAdd(d2 + 1, (unsigned long long)d_tot);                                          \
+      atomicAdd(d2 + 2, (unsigned long long)m_it);                                           \
+      atomicAdd(d2 + 3, (unsigned long long)m_act);                                          \
+      atomicAdd(d2 + 4, 1ull);                                                               \
+    }                                                                                        \
+  }
+#else
+#define LANE_DIAG_INIT uint64_t d_moves = 0;
+#define LANE_DIAG_ITER(active)
+#define LANE_DIAG_END (void)d_moves;
+#endif
+
+// The message words of block `blk` of the current job (rb holds it, prefetched).
+__device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const RawBlock& rb,
+                                           uint32_t (&W)[16]) {
+  if (64ull * blk >= jb.prefix) {
+    raw_to_words(rb, W);
+    if (rb.valid < 64) {
+      pad_words(rb.valid, W);
+      if (jb.fin && blk + 1 == jb.nblocks) {
+        const uint64_t bits = (jb.consumed + jb.L) * 8ull;
+        W[14] = (uint32_t)(bits >> 32);
+        W[15] = (uint32_t)bits;
+      }
+    }
+  } else {
+    sha_load_slow(jb, blk, W);  // head block of a continued chunk (once per segment)
+  }
+}
+
+// The region whose next job is the longest (longest-first across regions, so the last jobs
+// anywhere are short ones; ties: the first from `start` on), or R if every region is empty.
+// Called by a whole wave (some lanes may have left per-lane mode already); three dependent
+// loads per region, a few times per wave. (Picking the region with the most jobs left instead
+// ended configs[2]'s per-lane mode 2.3 ms after the median wave: regions left with few but
+// long jobs were found last.)
+__device__ uint32_t pick_region(const ShaArgs& a, uint32_t R, uint32_t start) {
+  const uint64_t act = __ballot(1);
+  const uint32_t nact = (uint32_t)__popcll(act);
+  const uint32_t rank =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  start %= R;
+  uint64_t key = 0;
+  for (uint32_t r = rank; r < R; r += nact) {
+    const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
+    const uint64_t h = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h < n) {
+      const uint32_t len = (a.jinfo[a.rorder[o + h]] & ~kJobElig) + 1u;
+      const uint64_t dist = (r + R - start) % R;
+      const uint64_t k = ((uint64_t)len << 8) | (255u - dist);
+      key = k > key ? k : key;
+    }
+  }
+  uint64_t best = 0;
+  for (uint64_t m = act; m; m &= m - 1) {  // max over the active lanes
+    const int l = (int)__builtin_ctzll(m);
+    const uint64_t v =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), l) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, l);
+    best = v > best ? v : best;
+  }
+  return best ? (uint32_t)((start + 255u - (uint32_t)(best & 255u)) % R) : R;
+}
+
+#if BSG_LANE_PIPE
+// Per-lane mode: each lane hashes one chunk at a time from the longest-first queue. Starting
+// the next job is pipelined per lane, one memory step per block iteration, so no iteration
+// ever waits for more than the block prefetched in the one before:
+//   BSG_LANE_LEAD blocks before the end: pop a queue slot q (atomic) -> load j = order[q] ->
+//   load its LaneJob (k_lens) -> on the last block, prefetch the new job's first block
+//   instead of the past-the-end one, and switch jobs in registers.
+// All of these memory operations (and the deferred record store of the job that ended) are
+// issued before the block prefetch, so the wait for that prefetch at the top of the next
+// iteration covers them. Round 2 popped and set up the next job only when the last one ended:
+// the whole wave waited for an atomic and ~4 dependent loads per job switch of any lane,
+// ~20 % of configs[2]'s per-lane time (BSG_LANE_DIAG builds). A job that is
+// too short for the pipeline idles only its own lane until its successor is ready; continued
+// and open chunks (streaming) still take the synchronous sha_setup path.
+__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ShaJob jb;
+  jb.dbase = a.data;  // a readable address for the idle prefetch before the first job
+  jb.L = 0;
+  jb.prefix = 0;
+  jb.consumed = 0;
+  jb.nblocks = 0;
+  jb.fin = 1;
+  uint32_t st[8] = {};
+  RawBlock rb;
+#pragma unroll
+  for (int i = 0; i < 17; ++i) rb.r[i] = 0;
+  rb.sel = 0;
+  rb.valid = 0;
+  bool act = false;
+  uint32_t blk = 0;
+  // next-job pipeline: 0 nothing, 1 slot popped (q next iteration), 2 job id loading (nj),
+  // 5 descriptor loading (ldn, job nj_d), 3 descriptor ready (ld, job ld_id), 4 queue exhausted
+  uint32_t stage = 0;
+  uint64_t q = 0, nj = 0, nj_d = 0, ld_id = 0;
+  // the descriptor as two 16-byte vectors (a struct got its words shuffled right after the
+  // load, which made the whole wave wait for it)
+  u32x4 ld0 = {0, 0, 0, 0}, ld1 = {0, 0, 0, 0}, ldn0 = ld0, ldn1 = ld0;
+  // a pop is one atomic per wave (the first active lane's); its result stays in that lane's
+  // register until the next iteration, where each popping lane adds its rank
+  uint64_t pop_base = 0;
+  uint32_t pop_leader = 0, pop_rank = 0;
+  // the record of the last job that ended, stored in the next iteration
+  bool pend = false;
+  uint64_t p_id = 0, p_start = 0, p_len = 0;
+  uint32_t p_level = 0, p_stream = 0, pst[8] = {};
+  uint64_t tm0 = 0, tr0 = 0;
+  bool stamp = false;
+  // The wave's region (wave-uniform): its workgroup's (= its CU's) first, then, whenever it
+  // runs dry, the one whose next job is the longest. pop_off / pop_n: the last pop's region.
+  const uint32_t R = (uint32_t)a.reg->nregions;
+  uint32_t reg = blockIdx.x % R;
+  uint64_t reg_off = a.reg->off[reg], reg_n = a.reg->off[reg + 1] - reg_off;
+  uint64_t pop_off = reg_off, pop_n = reg_n;
+  bool all_done = false;
+  LANE_DIAG_INIT
+  for (;;) {
+    LANE_DIAG_ITER(act)
+    // Everything the last iteration issued (block prefetch, pipeline loads, the pop, the
+    // record store) has had a whole compression to land: wait for all of it here, once, so
+    // the compiler needs no wait further down.
+    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+    uint32_t W[16];
+    lane_words(jb, blk, rb, W);  // garbage on idle lanes (never used)
+    // pipeline steps whose loads landed (the wait above): 5 -> 3, 2 -> 5, 1 -> 2 / 0
+    bool dry = false;
+    if (stage == 5) {
+      ld0 = ldn0;
+      ld1 = ldn1;
+      ld_id = nj_d;
+      stage = 3;
+    } else if (stage == 2) {
+      nj_d = nj;  // its descriptor is loaded below
+      stage = 5;
+    } else if (stage == 1) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pop_base, pop_leader);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pop_base >> 32), pop_leader);
+      const uint64_t local = (((uint64_t)hi << 32) | lo) + pop_rank;
+      q = pop_off + local;
+      dry = local >= pop_n;
+      stage = dry ? 0u : 2u;  // its job id is loaded below; else the region ran dry
+    }
+    if (__ballot(dry) && !all_done && pop_off == reg_off) {
+      // the current region ran dry: move to the one with the most jobs left (wave-uniform,
+      // synchronous; a few times per wave)
+      reg = pick_region(a, R, reg + 1);
+      d_moves += 1;
+      if (reg >= R) {
+        all_done = true;
+      } else {
+        reg_off = a.reg->off[reg];
+        reg_n = a.reg->off[reg + 1] - reg_off;
+      }
+    }
+    const bool ld_ready = stage == 3;
+    bool need = stage == 0 && (!act || blk + BSG_LANE_LEAD >= jb.nblocks);
+    if (all_done) {  // every region is empty: lanes wanting a job are done
+      if (need) stage = 4;
+      need = false;
+    }
+    // The two lookups run on every lane, every iteration (lanes with nothing to look up
+    // re-read entry 0 or their last one): a load under a per-lane condition into a
+    // loop-carried value made hipcc merge the old and the new value by register copies that
+    // waited for the load at once.
+    {
+      const gu32x4* pd = reinterpret_cast<const gu32x4*>(reinterpret_cast<uintptr_t>(a.jdesc + nj_d));
+      ldn0 = pd[0];
+      ldn1 = pd[1];
+      nj = a.rorder[stage == 2 ? q : 0ull];
+    }
+    const uint64_t nm = __ballot(need);
+    if (nm) {  // wave-uniform
+      const uint32_t leader = __builtin_amdgcn_readfirstlane(lane);
+      if (lane == leader) {
+        // an address the compiler cannot prove uniform, so that its atomic optimiser leaves
+        // this one-lane atomic alone (it would broadcast the result at once, i.e. wait for it)
+        uint32_t z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        pop_base = atomicAdd(reinterpret_cast<unsigned long long*>(&a.reg->head[reg]) + z,
+                             (unsigned long long)__popcll(nm));
+      }
+      pop_leader = leader;
+      pop_off = reg_off;
+      pop_n = reg_n;
+      if (need) {
+        pop_rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
+        stage = 1;
+      }
+    }
+    if (pend) {
+      ChunkRec* r = a.out + p_id;
+      r->offset = p_start;
+      r->len = p_len;
+      r->level = p_level;
+      r->stream = p_stream;
+      uint32_t* ref = reinterpret_cast<uint32_t*>(r->ref);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ref[i] = __builtin_bswap32(pst[i]);
+      pend = false;
+    }
+    // prefetch: the current job's next block, or on its last block (or when idle) the next
+    // job's first block; otherwise the current job's past-the-end block (slack, never used)
+    const bool cont = act && blk + 1 < jb.nblocks;
+    // LaneJob words: dptr (0, 1), start (2, 3), len (4, 5), stream (6), meta (7)
+    const uint64_t ld_dptr = ((uint64_t)ld0.y << 32) | ld0.x;
+    const uint64_t ld_start = ((uint64_t)ld0.w << 32) | ld0.z;
+    const uint64_t ld_len = ((uint64_t)ld1.y << 32) | ld1.x;
+    const bool take = !cont && ld_ready && !(ld1.w & kLaneJobSlow);
+    raw_load(take ? reinterpret_cast<const uint8_t*>(ld_dptr) : jb.dbase,
+             take ? 0ull : 64ull * blk + 64, take ? 0u : jb.prefix, take ? ld_len : jb.L, rb);
+    if (act) sha256_compress(st, W);
+    if (act && ++blk == jb.nblocks) {
+      act = false;
+      if (jb.fin) {
+        pend = true;
+        p_id = jb.id;
+        p_start = jb.start;
+        p_len = jb.end - jb.start;
+        p_level = jb.level;
+        p_stream = jb.stream;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pst[i] = st[i];
+      } else {
+        sha_finish(a, jb, st);  // open chunk: midstate carry (streaming, one per stream)
+      }
+      if (stamp && !BSG_LANE_DIAG) {
+        a.ctr->diag2[1] = __builtin_amdgcn_s_memtime();
+        a.ctr->diag2[3] = __builtin_amdgcn_s_memrealtime();
+        a.ctr->diag2[0] = tm0;
+        a.ctr->diag2[2] = tr0;
+        a.ctr->diag2[4] = jb.nblocks;
+        stamp = false;
+      }
+    }
+    if (!act) {
+      if (take) {  // its first block is on its way into rb
+        jb.id = ld_id;
+        jb.start = ld_start;
+        jb.end = ld_start + ld_len;
+        jb.dbase = reinterpret_cast<const uint8_t*>(ld_dptr);
+        jb.L = ld_len;
+        jb.consumed = 0;
+        jb.prefix = 0;
+        jb.fin = 1;
+        jb.level = ld1.w & ~kLaneJobSlow;
+        jb.stream = ld1.z;
+        jb.nblocks = (uint32_t)((ld_len + 8) / 64 + 1);
+        st[0] = 0x6a09e667; st[1] = 0xbb67ae85; st[2] = 0x3c6ef372; st[3] = 0xa54ff53a;
+        st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
+        blk = 0;
+        act = true;
+        stage = 0;
+        stamp = (q == 0);  // diagnostic timing of region 0's longest per-lane job
+        if (stamp) {
+          tm0 = __builtin_amdgcn_s_memtime();
+          tr0 = __builtin_amdgcn_s_memrealtime();
+        }
+      } else if (ld_ready) {  // continued or open chunk: the full setup, synchronously (rare)
+        stage = 0;
+        if (sha_setup(a, ld_id, M, jb, st)) {
+          blk = 0;
+          if (jb.nblocks == 0) {
+            sha_finish(a, jb, st);
+          } else {
+            act = true;
+            if (jb.prefix == 0) raw_load(jb.dbase, 0, 0, jb.L, rb);
+          }
+        }
+      } else if (stage == 4 && !pend) {
+        break;
+      }
+    }
+  }
+  LANE_DIAG_END
+}
+
+#else  // BSG_LANE_PIPE == 0: round-2 form (experiment A/B)
 __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   const uint64_t nshort = a.ctr->nshort;
   ShaJob jb;
@@ -893,19 +1214,13 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   RawBlock rb;
   bool has = false, exhausted = false;
   uint32_t blk = 0;
-  uint64_t tm0 = 0, tr0 = 0;
-  bool stamp = false;
+  LANE_DIAG_INIT
   for (;;) {
     while (!has && !exhausted) {
       const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->job_head), 1ull);
       if (q >= nshort) {
         exhausted = true;
       } else if (sha_setup(a, a.order[q], M, jb, st)) {
-        stamp = (q == 0);  // diagnostic timing of the longest per-lane job
-        if (stamp) {
-          tm0 = __builtin_amdgcn_s_memtime();
-          tr0 = __builtin_amdgcn_s_memrealtime();
-        }
         blk = 0;
         if (jb.nblocks == 0) {
           sha_finish(a, jb, st);
@@ -916,39 +1231,19 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
       }
     }
     if (!has) break;
+    LANE_DIAG_ITER(true)
     uint32_t W[16];
-    const uint64_t o0 = 64ull * blk;
-    if (o0 >= jb.prefix) {
-      raw_to_words(rb, W);
-      if (rb.valid < 64) {
-        pad_words(rb.valid, W);
-        if (jb.fin && blk + 1 == jb.nblocks) {
-          const uint64_t bits = (jb.consumed + jb.L) * 8ull;
-          W[14] = (uint32_t)(bits >> 32);
-          W[15] = (uint32_t)bits;
-        }
-      }
-    } else {
-      sha_load_slow(jb, blk, W);  // head block of a continued chunk (once per segment)
-    }
-    // prefetch the next block, unconditionally (past the last block it reads slack bytes,
-    // which are never used): a branch here would make the compiler drain vmcnt at the join
-    raw_load(jb.dbase, o0 + 64, jb.prefix, jb.L, rb);
+    lane_words(jb, blk, rb, W);
+    raw_load(jb.dbase, 64ull * blk + 64, jb.prefix, jb.L, rb);
     sha256_compress(st, W);
     if (++blk == jb.nblocks) {
       sha_finish(a, jb, st);
       has = false;
-      if (stamp) {
-        a.ctr->diag2[1] = __builtin_amdgcn_s_memtime();
-        a.ctr->diag2[3] = __builtin_amdgcn_s_memrealtime();
-        a.ctr->diag2[0] = tm0;
-        a.ctr->diag2[2] = tr0;
-        a.ctr->diag2[4] = jb.nblocks;
-        stamp = false;
-      }
     }
   }
+  LANE_DIAG_END
 }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Wave-per-chunk path for the longest chunks. A SHA-256 chain is serial, so a batch's wall time
@@ -967,9 +1262,14 @@ __device__ __forceinline__ uint32_t lpt_bucket(const Counters* ctr, uint32_t nbl
   return b < (uint64_t)kLptBuckets ? (uint32_t)b : (uint32_t)(kLptBuckets - 1);
 }
 
-// Job info from k_lens (jinfo): nblocks | eligible << 31; kNoJob for ids without a job.
-constexpr uint32_t kNoJob = 0xffffffffu;
-constexpr uint32_t kJobElig = 0x80000000u;
+// Region (0 .. R-1) of a per-lane job by the address of its first data byte.
+__device__ __forceinline__ uint32_t job_region(const ShaArgs& a, uint64_t dptr, uint32_t R) {
+  const int64_t o = (int64_t)(dptr - reinterpret_cast<uint64_t>(a.data));
+  if (o <= 0 || R <= 1) return 0;
+  const uint64_t r = ((uint64_t)o * R) / (a.span ? a.span : 1);
+  return r < R ? (uint32_t)r : R - 1;
+}
+
 
 // Counting sort of the jobs on their LPT bucket, aggregated in LDS: pass 1 (SCATTER = false)
 // counts jobs (and wave-eligible jobs) per bucket, one global atomic per non-empty bucket per
@@ -1018,8 +1318,12 @@ __global__ __launch_bounds__(256) void k_order(ShaArgs a) {
     }
     __syncthreads();
     if (SCATTER && info != kNoJob) {
-      if (is_long) a.long_list[h1[b] + rank] = j;
-      else a.order[h0[b] + rank] = j;
+      if (is_long) {
+        a.long_list[h1[b] + rank] = j;
+      } else {
+        a.order[h0[b] + rank] = j;
+        a.oreg[h0[b] + rank] = (uint8_t)job_region(a, a.jdesc[j].dptr, (uint32_t)a.reg->nregions);
+      }
     }
     __syncthreads();
   }
@@ -1047,6 +1351,104 @@ __device__ __forceinline__ uint32_t block_scan4(uint32_t (&v)[4], uint32_t (&pre
 #pragma unroll
   for (int i = 0; i < 4; ++i) { pre[i] = p; p += v[i]; }
   return total;
+}
+
+// ---- per-lane jobs regrouped by region, longest first within each (see Regions) ----------
+// The LPT order (a.order, nshort jobs) is cut into kRegionSegs segments; k_rcount counts each
+// segment's jobs per region, k_rscan turns the counts into each segment's offset within its
+// region, k_rtotal lays the regions out, and k_rscatter moves every job to
+// rorder[off[region] + its segment's offset + its rank], walking its segment in order, so each
+// region keeps the LPT order (up to the order inside one 256-job tile).
+__device__ __forceinline__ uint64_t seg_len(uint64_t n) {
+  return (n + kRegionSegs - 1) / kRegionSegs;
+}
+
+__global__ __launch_bounds__(256) void k_rcount(ShaArgs a) {
+  __shared__ uint32_t hist[kMaxRegions];
+  if (a.ctr->overflow || a.ctr->error || a.ctr->nchunks > a.chunk_cap) return;
+  const uint64_t n = a.ctr->nshort, L = seg_len(n);
+  const uint32_t t = threadIdx.x;
+  hist[t] = 0;
+  __syncthreads();
+  const uint64_t lo = blockIdx.x * L, hi = min(n, lo + L);
+  for (uint64_t i = lo + t; i < hi; i += 256) atomicAdd(&hist[a.oreg[i]], 1u);
+  __syncthreads();
+  a.reg->cnt[blockIdx.x * kMaxRegions + t] = hist[t];
+}
+
+__global__ __launch_bounds__(kRegionSegs) void k_rscan(ShaArgs a) {
+  __shared__ uint32_t wsum[kRegionSegs / 64];
+  if (a.ctr->overflow || a.ctr->error || a.ctr->nchunks > a.chunk_cap) return;
+  const uint32_t r = blockIdx.x, t = threadIdx.x;  // region r, segment t
+  if (r >= a.reg->nregions) return;
+  uint32_t* c = a.reg->cnt + t * kMaxRegions + r;
+  const uint32_t v = *c;
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((t & 63) >= (uint32_t)o) x += y;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (uint32_t w = 0; w < kRegionSegs / 64; ++w) {
+    if (w < (t >> 6)) base += wsum[w];
+    tot += wsum[w];
+  }
+  *c = base + x - v;  // exclusive: segment t's offset within region r
+  if (t == 0) a.reg->head[r] = tot;  // the region's size, until k_rtotal
+}
+
+__global__ __launch_bounds__(kMaxRegions) void k_rtotal(ShaArgs a) {
+  __shared__ uint64_t wsum[kMaxRegions / 64];
+  if (a.ctr->overflow || a.ctr->error || a.ctr->nchunks > a.chunk_cap) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t R = (uint32_t)a.reg->nregions;
+  const uint64_t v = t < R ? a.reg->head[t] : 0;
+  uint64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o);
+    if ((t & 63) >= (uint32_t)o) x += y;
+  }
+  if ((t & 63) == 63) wsum[t >> 6] = x;
+  __syncthreads();
+  uint64_t base = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) base += wsum[w];
+  __syncthreads();
+  a.reg->off[t] = t < R ? base + x - v : a.ctr->nshort;
+  if (t == 0) {
+    a.reg->off[kMaxRegions] = a.ctr->nshort;
+    a.reg->rr = 0;
+  }
+  a.reg->head[t] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_rscatter(ShaArgs a) {
+  __shared__ uint64_t base[kMaxRegions];
+  __shared__ uint32_t tc[kMaxRegions];
+  if (a.ctr->overflow || a.ctr->error || a.ctr->nchunks > a.chunk_cap) return;
+  const uint64_t n = a.ctr->nshort, L = seg_len(n);
+  const uint32_t t = threadIdx.x;
+  base[t] = a.reg->off[t] + a.reg->cnt[blockIdx.x * kMaxRegions + t];
+  tc[t] = 0;
+  __syncthreads();
+  const uint64_t lo = blockIdx.x * L, hi = min(n, lo + L);
+  for (uint64_t tile = lo; tile < hi; tile += 256) {
+    const uint64_t i = tile + t;
+    uint32_t r = 0, rank = 0;
+    uint64_t j = 0;
+    if (i < hi) {
+      r = a.oreg[i];
+      j = a.order[i];
+      rank = atomicAdd(&tc[r], 1u);
+    }
+    __syncthreads();
+    if (i < hi) a.rorder[base[r] + rank] = j;
+    __syncthreads();
+    base[t] += tc[t];
+    tc[t] = 0;
+    __syncthreads();
+  }
 }
 
 // Splits the jobs between the SHA-256 paths and lays out both queues, longest first.
@@ -1125,6 +1527,10 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
     a.ctr->long_buckets = nlb;
     a.ctr->nlong = nlong;
     a.ctr->nshort = nshort;
+    // regions of <= kRegionBytes (one per several CUs), each with enough jobs to balance
+    const uint64_t rmax = min((uint64_t)kMaxRegions, max((uint64_t)a.waves / 16, (uint64_t)1));
+    const uint64_t rspan = (a.span + kRegionBytes - 1) / kRegionBytes;
+    a.reg->nregions = min(min(rmax, rspan), max((uint64_t)nshort / kMinRegionJobs, (uint64_t)1));
     a.ctr->long_thresh = mx > (uint64_t)nlb * w ? mx - (uint64_t)nlb * w : 0;  // diagnostic
     a.ctr->nlong_grp = n8;
     a.ctr->tickets_grp = t8;
@@ -1148,6 +1554,15 @@ __global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
       // continued chunks (a head from hist) stay per-lane
       if (jb.prefix == 0) mx = max(mx, (uint64_t)jb.nblocks);
       info = min(jb.nblocks, ~kJobElig) | (jb.prefix == 0 ? kJobElig : 0u);
+      LaneJob d;
+      d.dptr = reinterpret_cast<uint64_t>(jb.dbase);
+      d.start = jb.start;
+      d.len = jb.L;
+      d.stream = jb.stream;
+      // per-lane mode starts a fresh final chunk from this alone; a continued chunk (midstate,
+      // head bytes) or an open one (midstate out) takes sha_setup
+      d.meta = jb.level | ((jb.fin && jb.prefix == 0 && jb.consumed == 0) ? 0u : kLaneJobSlow);
+      a.jdesc[j] = d;
     }
     a.jinfo[j] = info;
   }
@@ -1544,6 +1959,10 @@ hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, 
   hipLaunchKernelGGL(k_order<false>, dim3(grid), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_order<true>, dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_rcount, dim3(kRegionSegs), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_rscan, dim3(kMaxRegions), dim3(kRegionSegs), 0, s, a);
+  hipLaunchKernelGGL(k_rtotal, dim3(1), dim3(kMaxRegions), 0, s, a);
+  hipLaunchKernelGGL(k_rscatter, dim3(kRegionSegs), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -85,6 +85,12 @@ struct ShaArgs {
   uint32_t* bucket_loff;    // [kLptBuckets] long-list offsets
   uint32_t* jinfo;          // [chunk_cap + nstreams] per job, from k_lens: nblocks | eligible
                             // << 31, or kNoJob (no job: a short open chunk carried as bytes)
+  LaneJob* jdesc;           // [chunk_cap + nstreams] per job, from k_lens: what per-lane mode
+                            // needs to start it without sha_setup's dependent loads
+  Regions* reg;             // per-lane region queues (see Regions)
+  uint8_t* oreg;            // [chunk_cap + nstreams] region of order[i] (k_order)
+  uint64_t* rorder;         // [chunk_cap + nstreams] per-lane jobs by region, longest first
+  uint64_t span;            // bytes from data to the end of the last stream (regions)
   int long_mode;            // 0 auto, 1 per-lane only, 2 wave mode only (experiments)
   uint32_t waves;           // waves of the k_sha grid (4 per CU)
 };
