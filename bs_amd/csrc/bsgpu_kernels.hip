@@ -937,13 +937,29 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
 #define LANE_DIAG_END (void)d_moves;
 #endif
 
-// The message words of block `blk` of the current job (rb holds it, prefetched).
+// Tail block, cheaper form for the per-lane loop: words before the one holding byte `valid`
+// stay, that word keeps its valid bytes and gets the 0x80, later words are zero (valid -1: a
+// block of padding only).
+__device__ __forceinline__ void pad_words_lane(int32_t valid, uint32_t (&W)[16]) {
+  const int32_t q0 = valid >> 2;  // arithmetic: -1 for valid == -1
+  const uint32_t b = 8u * ((uint32_t)valid & 3u);
+  const uint32_t keep = ~(0xffffffffu >> b), pad = 0x80000000u >> b;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const uint32_t t = (W[q] & keep) | pad;
+    W[q] = q < q0 ? W[q] : (q == q0 ? t : 0u);
+  }
+}
+
+// The message words of block `blk` of the current job (rb holds it, prefetched). Idle lanes
+// (act false) skip the tail handling: their rb is a past-the-end block, and taking the tail
+// branch for them would run it for the whole wave in nearly every iteration.
 __device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const RawBlock& rb,
-                                           uint32_t (&W)[16]) {
+                                           bool act, uint32_t (&W)[16]) {
   if (64ull * blk >= jb.prefix) {
     raw_to_words(rb, W);
-    if (rb.valid < 64) {
-      pad_words(rb.valid, W);
+    if (act && rb.valid < 64) {
+      pad_words_lane(rb.valid, W);
       if (jb.fin && blk + 1 == jb.nblocks) {
         const uint64_t bits = (jb.consumed + jb.L) * 8ull;
         W[14] = (uint32_t)(bits >> 32);
@@ -1052,7 +1068,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
     // the compiler needs no wait further down.
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
     uint32_t W[16];
-    lane_words(jb, blk, rb, W);  // garbage on idle lanes (never used)
+    lane_words(jb, blk, rb, act, W);  // garbage on idle lanes (never used)
     // pipeline steps whose loads landed (the wait above): 5 -> 3, 2 -> 5, 1 -> 2 / 0
     bool dry = false;
     if (stage == 5) {
@@ -1233,7 +1249,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
     if (!has) break;
     LANE_DIAG_ITER(true)
     uint32_t W[16];
-    lane_words(jb, blk, rb, W);
+    lane_words(jb, blk, rb, true, W);
     raw_load(jb.dbase, 64ull * blk + 64, jb.prefix, jb.L, rb);
     sha256_compress(st, W);
     if (++blk == jb.nblocks) {
