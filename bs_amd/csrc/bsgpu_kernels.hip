@@ -1005,6 +1005,53 @@ __device__ uint32_t pick_region(const ShaArgs& a, uint32_t R, uint32_t start) {
   return best ? (uint32_t)((start + 255u - (uint32_t)(best & 255u)) % R) : R;
 }
 
+#ifndef BSG_REGION_POLL
+#define BSG_REGION_POLL 8      // a wave compares its region's progress with the others' every
+#endif                         // this many pops (0: only when its region runs dry)
+#ifndef BSG_REGION_LAG
+#define BSG_REGION_LAG 3       // ... and moves if it is this many % of its jobs ahead of the
+#endif                         // region furthest behind
+
+// Regions are drained longest job first, so the share of a region's jobs already taken says how
+// far down its length order it is. Returns the region furthest behind if `cur` is more than
+// BSG_REGION_LAG % ahead of it, else `cur`. One round of loads; called by a whole wave.
+__device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
+  const uint64_t act = __ballot(1);
+  const uint32_t nact = (uint32_t)__popcll(act);
+  const uint32_t rank =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  uint64_t key = 0;       // (2^20 - share taken) << 8 | (255 - distance from cur)
+  uint32_t mine = 0;      // cur's share taken (2^20 = all), on the lane that read it
+  bool has_mine = false;
+  for (uint32_t r = rank; r < R; r += nact) {
+    const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
+    const uint64_t h = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t taken = n ? (uint32_t)(min(h, n) * (1ull << 20) / n) : (1u << 20);
+    if (r == cur) {
+      mine = taken;
+      has_mine = true;
+    }
+    if (h < n) {
+      const uint64_t k = ((uint64_t)((1u << 20) - taken) << 8) | (255u - (r + R - cur) % R);
+      key = k > key ? k : key;
+    }
+  }
+  uint64_t best = 0;
+  uint32_t cur_taken = 0;
+  for (uint64_t m = act; m; m &= m - 1) {
+    const int l = (int)__builtin_ctzll(m);
+    const uint64_t v =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), l) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, l);
+    best = v > best ? v : best;
+    if (__builtin_amdgcn_readlane((int)has_mine, l)) cur_taken = (uint32_t)__builtin_amdgcn_readlane((int)mine, l);
+  }
+  if (!best) return cur;
+  const uint32_t behind_taken = (1u << 20) - (uint32_t)(best >> 8);
+  if (cur_taken <= behind_taken + (uint32_t)(((1ull << 20) * BSG_REGION_LAG) / 100)) return cur;
+  return (cur + 255u - (uint32_t)(best & 255u)) % R;
+}
+
 #if BSG_LANE_PIPE
 // Per-lane mode: each lane hashes one chunk at a time from the longest-first queue. Starting
 // the next job is pipelined per lane, one memory step per block iteration, so no iteration
@@ -1060,6 +1107,8 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   uint64_t reg_off = a.reg->off[reg], reg_n = a.reg->off[reg + 1] - reg_off;
   uint64_t pop_off = reg_off, pop_n = reg_n;
   bool all_done = false;
+  uint32_t npops = 0;     // pops by this wave (wave-uniform)
+  bool poll = false;
   LANE_DIAG_INIT
   for (;;) {
     LANE_DIAG_ITER(act)
@@ -1099,6 +1148,17 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
         reg_n = a.reg->off[reg + 1] - reg_off;
       }
     }
+    if (BSG_REGION_POLL && poll && !all_done && R > 1) {
+      // keep the regions level: move to the one furthest behind if this one is well ahead
+      poll = false;
+      const uint32_t r2 = behind_region(a, R, reg);
+      if (r2 != reg) {
+        reg = r2;
+        reg_off = a.reg->off[reg];
+        reg_n = a.reg->off[reg + 1] - reg_off;
+        d_moves += 1;
+      }
+    }
     const bool ld_ready = stage == 3;
     bool need = stage == 0 && (!act || blk + BSG_LANE_LEAD >= jb.nblocks);
     if (all_done) {  // every region is empty: lanes wanting a job are done
@@ -1129,6 +1189,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
       pop_leader = leader;
       pop_off = reg_off;
       pop_n = reg_n;
+      if (BSG_REGION_POLL && ++npops % (BSG_REGION_POLL ? BSG_REGION_POLL : 1) == 0) poll = true;
       if (need) {
         pop_rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32),
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
