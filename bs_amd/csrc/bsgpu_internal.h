@@ -144,12 +144,16 @@ struct Regions {
   uint64_t off[kMaxRegions + 1];             // region r's jobs: rorder[off[r] .. off[r + 1])
   uint64_t pad2_[7];
   uint32_t cnt[kRegionSegs * kMaxRegions];   // per segment and region: count, then offset
-  uint64_t wdbg[1024 * 4];                   // BSG_LANE_DIAG builds: per k_sha wave, per-lane
-                                             // mode entry / exit time, region moves, iterations
+  uint64_t wdbg[1024 * 8];                   // BSG_LANE_DIAG builds: per k_sha wave, per-lane
+                                             // mode entry / exit time, region moves, iterations,
+                                             // last wave-mode ticket, its start / end, blocks
 };
 
 constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave path below 64 KiB
-constexpr uint32_t kSolo = 8;    // wave mode: the kSolo longest jobs run one per wave,
+#ifndef BSG_SOLO
+#define BSG_SOLO 16  // configs[2]: the 9th-16th longest jobs on group tickets (1.40 us per
+#endif           // block against 1.19 solo) ended 0.5 ms after the longest
+constexpr uint32_t kSolo = BSG_SOLO;  // wave mode: the kSolo longest jobs run one per wave,
 constexpr uint32_t kGroup = 8;   // the next ones kGroup per wave (one banked lane pair each)
 constexpr uint32_t kPairGroup = 32;  // then (optionally) 32 per wave, one lane pair each
 constexpr int kLongRow = 68;               // LDS words per K+W row (64 + pad: conflict-free b128)

@@ -27,15 +27,18 @@
 #define BSG_BANK_ROUNDS 1
 #endif
 // Wave-mode tiers (k_bucket_scan), in percent of the longest job's blocks: jobs of at least
-// BSG_TLEN_PCT run on solo / group tickets (8 jobs per wave), jobs of BSG_PAIR_PCT up to that
-// on pair tickets (32 per wave, one skewed lane pair each, ring fills every 2 blocks), the rest
-// per lane. Measured on configs[2]: 56 / 30 gives 761-767 GiB/s against
-// 669-719 for 43 / off (the round-1 setting); configs[1] is unchanged (84.2-84.6).
+// BSG_TLEN_PCT run on solo / group tickets (the kSolo longest one per wave, then 8 per wave),
+// jobs of BSG_PAIR_PCT up to that on pair tickets (32 per wave, one skewed lane pair each, ring
+// fills every 2 blocks), the rest per lane. A pair job's block takes ~2.27 us under load
+// against the solo chain's 1.19, so pair jobs above ~0.52 of the longest end after it; with
+// the faster per-lane mode (regions, round 2) per-lane jobs may reach 0.34 of it. Measured on
+// configs[2]: 50 / 34 with 16 solo tickets 888 GiB/s, 56 / 30 with 8 (the
+// earlier setting) 831 on the same box; configs[1] unchanged.
 #ifndef BSG_TLEN_PCT
-#define BSG_TLEN_PCT 56
+#define BSG_TLEN_PCT 50
 #endif
 #ifndef BSG_PAIR_PCT
-#define BSG_PAIR_PCT 30
+#define BSG_PAIR_PCT 34
 #endif
 // With the octet chains (round 2) a lightly loaded launch — all its blocks are less than a
 // tenth of what the chip's lanes hash while the longest chain runs — ends on the pair tickets
@@ -895,8 +898,11 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
 #define BSG_LANE_PIPE 1
 #endif
 #ifndef BSG_LANE_LEAD
-#define BSG_LANE_LEAD 4
+#define BSG_LANE_LEAD 4  // iterations before a job's end at which its successor is popped
 #endif
+#ifndef BSG_LANE_BPI
+#define BSG_LANE_BPI 2   // blocks per per-lane iteration: the job-switch and queue logic runs
+#endif                   // once per this many compressions
 
 #if BSG_LANE_DIAG
 // experiment: diag2[] = sums over waves of (0), lane-mode cycles, iterations, active
@@ -913,10 +919,10 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
     const uint64_t d_tot = __builtin_amdgcn_s_memtime() - d_t0;                              \
     const uint32_t wid = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);                \
     if ((threadIdx.x & 63u) == 0 && wid < 1024) {                                            \
-      a.reg->wdbg[4 * wid + 0] = d_rt0;                                                      \
-      a.reg->wdbg[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();                           \
-      a.reg->wdbg[4 * wid + 2] = d_moves;                                                    \
-      a.reg->wdbg[4 * wid + 3] = d_it;                                                       \
+      a.reg->wdbg[8 * wid + 0] = d_rt0;                                                      \
+      a.reg->wdbg[8 * wid + 1] = __builtin_amdgcn_s_memrealtime();                           \
+      a.reg->wdbg[8 * wid + 2] = d_moves;                                                    \
+      a.reg->wdbg[8 * wid + 3] = d_it;                                                       \
     }                                                                                        \
     uint64_t m_it = d_it, m_act = d_act;                                                     \
     for (int o = 32; o > 0; o >>= 1) {                                                       \
@@ -1067,6 +1073,7 @@ __device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
 // too short for the pipeline idles only its own lane until its successor is ready; continued
 // and open chunks (streaming) still take the synchronous sha_setup path.
 __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
+  constexpr int kBPI = BSG_LANE_BPI;  // blocks per iteration (per lane)
   const uint32_t lane = threadIdx.x & 63u;
   ShaJob jb;
   jb.dbase = a.data;  // a readable address for the idle prefetch before the first job
@@ -1076,11 +1083,14 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   jb.nblocks = 0;
   jb.fin = 1;
   uint32_t st[8] = {};
-  RawBlock rb;
+  RawBlock rb[kBPI];
 #pragma unroll
-  for (int i = 0; i < 17; ++i) rb.r[i] = 0;
-  rb.sel = 0;
-  rb.valid = 0;
+  for (int b = 0; b < kBPI; ++b) {
+#pragma unroll
+    for (int i = 0; i < 17; ++i) rb[b].r[i] = 0;
+    rb[b].sel = 0;
+    rb[b].valid = 0;
+  }
   bool act = false;
   uint32_t blk = 0;
   // next-job pipeline: 0 nothing, 1 slot popped (q next iteration), 2 job id loading (nj),
@@ -1116,8 +1126,10 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
     // record store) has had a whole compression to land: wait for all of it here, once, so
     // the compiler needs no wait further down.
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
-    uint32_t W[16];
-    lane_words(jb, blk, rb, act, W);  // garbage on idle lanes (never used)
+    uint32_t W[kBPI][16];
+#pragma unroll
+    for (int b = 0; b < kBPI; ++b)  // garbage on idle lanes and past a job's end (never used)
+      lane_words(jb, blk + b, rb[b], act && blk + b < jb.nblocks, W[b]);
     // pipeline steps whose loads landed (the wait above): 5 -> 3, 2 -> 5, 1 -> 2 / 0
     bool dry = false;
     if (stage == 5) {
@@ -1160,7 +1172,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
       }
     }
     const bool ld_ready = stage == 3;
-    bool need = stage == 0 && (!act || blk + BSG_LANE_LEAD >= jb.nblocks);
+    bool need = stage == 0 && (!act || blk + kBPI * BSG_LANE_LEAD >= jb.nblocks);
     if (all_done) {  // every region is empty: lanes wanting a job are done
       if (need) stage = 4;
       need = false;
@@ -1207,18 +1219,24 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
       for (int i = 0; i < 8; ++i) ref[i] = __builtin_bswap32(pst[i]);
       pend = false;
     }
-    // prefetch: the current job's next block, or on its last block (or when idle) the next
-    // job's first block; otherwise the current job's past-the-end block (slack, never used)
-    const bool cont = act && blk + 1 < jb.nblocks;
+    // prefetch: the current job's next blocks, or in its last iteration (or when idle) the
+    // next job's first ones; otherwise past-the-end blocks (slack, never used)
+    const bool cont = act && blk + kBPI < jb.nblocks;
     // LaneJob words: dptr (0, 1), start (2, 3), len (4, 5), stream (6), meta (7)
     const uint64_t ld_dptr = ((uint64_t)ld0.y << 32) | ld0.x;
     const uint64_t ld_start = ((uint64_t)ld0.w << 32) | ld0.z;
     const uint64_t ld_len = ((uint64_t)ld1.y << 32) | ld1.x;
     const bool take = !cont && ld_ready && !(ld1.w & kLaneJobSlow);
-    raw_load(take ? reinterpret_cast<const uint8_t*>(ld_dptr) : jb.dbase,
-             take ? 0ull : 64ull * blk + 64, take ? 0u : jb.prefix, take ? ld_len : jb.L, rb);
-    if (act) sha256_compress(st, W);
-    if (act && ++blk == jb.nblocks) {
+#pragma unroll
+    for (int b = 0; b < kBPI; ++b)
+      raw_load(take ? reinterpret_cast<const uint8_t*>(ld_dptr) : jb.dbase,
+               take ? 64ull * b : 64ull * (blk + kBPI + b), take ? 0u : jb.prefix,
+               take ? ld_len : jb.L, rb[b]);
+#pragma unroll
+    for (int b = 0; b < kBPI; ++b)
+      if (act && blk + b < jb.nblocks) sha256_compress(st, W[b]);
+    blk += kBPI;
+    if (act && blk >= jb.nblocks) {
       act = false;
       if (jb.fin) {
         pend = true;
@@ -1272,7 +1290,9 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
             sha_finish(a, jb, st);
           } else {
             act = true;
-            if (jb.prefix == 0) raw_load(jb.dbase, 0, 0, jb.L, rb);
+#pragma unroll
+            for (int b = 0; b < kBPI; ++b)  // block 0 of a continued chunk: sha_load_slow
+              if (64u * b >= jb.prefix) raw_load(jb.dbase, 64ull * b, jb.prefix, jb.L, rb[b]);
           }
         }
       } else if (stage == 4 && !pend) {
@@ -1712,6 +1732,9 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     tr0 = __builtin_amdgcn_s_memrealtime();
   }
   const uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
+#if BSG_LANE_DIAG
+  const uint64_t d_tk0 = __builtin_amdgcn_s_memrealtime();
+#endif
 #if BSG_BANK_ROUNDS
   // Pair tickets: skewed lane pairs (2p: E, 2p+1: A). Solo and group tickets: skewed octets
   // (one chain per 8 lanes, E quad at positions 0-3, A quad at 4-7; 8 VALU per round against
@@ -1799,6 +1822,18 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   st[7] = (uint32_t)__shfl((int)hs[1], pe);
   st[4] = (uint32_t)__shfl((int)hs[2], pe);
   st[5] = (uint32_t)__shfl((int)hs[3], pe);
+#endif
+#if BSG_LANE_DIAG
+  {
+    const uint32_t wid = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && wid < 1024) {
+      a.reg->wdbg[8 * wid + 4] = t + 1;
+      a.reg->wdbg[8 * wid + 5] = d_tk0;
+      a.reg->wdbg[8 * wid + 6] = rt1;
+      a.reg->wdbg[8 * wid + 7] = (uint64_t)nmax | ((uint64_t)(solo ? 0 : pairs ? 2 : 1) << 32);
+    }
+  }
 #endif
   if (vb && (lane & (B - 1u)) == 0) {
     sha_finish(a, jb, st);

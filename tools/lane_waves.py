@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bs_amd import bsgpu  # noqa: E402
 
-REGIONS_BYTES = 8 * (8 + 256 + 257 + 7) + 4 * 256 * 256 + 8 * 4096
+REGIONS_BYTES = 8 * (8 + 256 + 257 + 7) + 4 * 256 * 256 + 8 * 8192
 
 
 def main():
@@ -36,7 +36,7 @@ def main():
     t0 = int(t[0])
     R = int(raw[0])
     off = raw[8 + 256: 8 + 256 + 257]
-    w = raw[-4096:].reshape(1024, 4).astype(np.int64)
+    w = raw[-8192:].reshape(1024, 8).astype(np.int64)
     ent = (w[:, 0] - t0) * 0.01  # us (100 MHz realtime)
     ext = (w[:, 1] - t0) * 0.01
     mv, it = w[:, 2], w[:, 3]
@@ -49,6 +49,21 @@ def main():
     print("latest waves: id entry exit moves iters")
     for i in late:
         print(f"  {i:5d} {ent[i]:9.1f} {ext[i]:9.1f} {mv[i]:4d} {it[i]:6d}")
+    tk = w[:, 4] > 0
+    tend = (w[:, 6] - t0) * 0.01
+    tstart = (w[:, 5] - t0) * 0.01
+    kind = w[:, 7] >> 32
+    nb = w[:, 7] & 0xffffffff
+    print(f"ticket waves {tk.sum()}: latest ticket ends (wave, ticket, kind 0 solo 1 group 2 pair,"
+          " start us, end us, longest job blocks, us per block)")
+    for i in np.argsort(np.where(tk, tend, -1))[-16:]:
+        print(f"  {i:5d} {w[i, 4] - 1:5d} {kind[i]} {tstart[i]:8.1f} {tend[i]:9.1f} {nb[i]:6d} "
+              f"{(tend[i] - tstart[i]) / max(nb[i], 1):.3f}")
+    for k, name in ((0, "solo"), (1, "group"), (2, "pair")):
+        m = tk & (kind == k)
+        if m.any():
+            print(f"{name}: {m.sum()} tickets, end max {tend[m].max():.0f} us, us/block "
+                  f"median {np.median((tend[m] - tstart[m]) / np.maximum(nb[m], 1)):.3f}")
     hist, edges = np.histogram(ext, bins=20)
     print("exit histogram (us):", " ".join(f"{int(e)}:{h}" for e, h in zip(edges[:-1], hist)))
     eng.close()
