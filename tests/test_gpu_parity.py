@@ -368,3 +368,28 @@ def test_sha_path_forced(gpu, oracle, table, mode, monkeypatch):
             one = oracle.split(table, a, bits=bits, min_size=mn)
             assert as_tuples(ch[k:k + int(counts[i])]) == as_tuples(one), (mode, bits, i)
             k += int(counts[i])
+
+
+@pytest.mark.parametrize("carry_cap", [None, 0])
+def test_streaming_big_tiles_regions(gpu, oracle, table, carry_cap):
+    """Tiles over 1 GiB, so k_sha's per-lane jobs split into two address regions while the
+    open chunk of each tile is continued in the next (carry_cap 0: from a SHA-256 midstate, a
+    per-lane job on the synchronous setup path inside the region queues)."""
+    from bs_amd.synth import splitmix_array
+    n = (9 << 28) + 12345                 # 2.25 GiB + a ragged end
+    tile = (9 << 27) + 3                  # 1.125 GiB tiles
+    d = splitmix_array(0xB16, n)
+    want = oracle.split(table, d, bits=16, min_size=1024)
+    w = gpu.StreamingSplitter(bits=16, min_size=1024, tile=tile, carry_cap=carry_cap)
+    got = []
+    mv = memoryview(d)
+    for i in range(0, n, 256 << 20):
+        w.write(mv[i:i + (256 << 20)])
+        got.append(w.drain())
+    w.close()
+    got.append(w.drain())
+    w.free()
+    ch = np.concatenate(got)
+    assert len(ch) == len(want)
+    assert (ch["offset"] == want["offset"]).all() and (ch["len"] == want["len"]).all()
+    assert (ch["ref"] == want["ref"]).all() and (ch["level"] == want["level"]).all()
