@@ -88,7 +88,7 @@ struct Params {
 struct Counters {
   uint64_t ncand;              // total candidates (from the strip-count scan)
   uint64_t nchunks;            // total boundaries = finalized chunks
-  uint64_t job_head;           // SHA-256 dynamic work queue head
+  uint64_t job_head;           // unused (round 1: the per-lane queue head; now Regions::head)
   uint64_t overflow;           // candidate buffer too small (host grows and re-runs)
   uint64_t error;              // device-side sanity check failed (bug guard; run is invalid)
   uint64_t max_nblocks;        // longest SHA-256 job in blocks (k_lens)

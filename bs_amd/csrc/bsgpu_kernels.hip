@@ -894,9 +894,6 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
 #ifndef BSG_LANE_DIAG
 #define BSG_LANE_DIAG 0
 #endif
-#ifndef BSG_LANE_PIPE
-#define BSG_LANE_PIPE 1
-#endif
 #ifndef BSG_LANE_LEAD
 #define BSG_LANE_LEAD 4  // iterations before a job's end at which its successor is popped
 #endif
@@ -1058,20 +1055,19 @@ __device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
   return (cur + 255u - (uint32_t)(best & 255u)) % R;
 }
 
-#if BSG_LANE_PIPE
-// Per-lane mode: each lane hashes one chunk at a time from the longest-first queue. Starting
-// the next job is pipelined per lane, one memory step per block iteration, so no iteration
-// ever waits for more than the block prefetched in the one before:
-//   BSG_LANE_LEAD blocks before the end: pop a queue slot q (atomic) -> load j = order[q] ->
-//   load its LaneJob (k_lens) -> on the last block, prefetch the new job's first block
-//   instead of the past-the-end one, and switch jobs in registers.
-// All of these memory operations (and the deferred record store of the job that ended) are
-// issued before the block prefetch, so the wait for that prefetch at the top of the next
-// iteration covers them. Round 2 popped and set up the next job only when the last one ended:
-// the whole wave waited for an atomic and ~4 dependent loads per job switch of any lane,
-// ~20 % of configs[2]'s per-lane time (BSG_LANE_DIAG builds). A job that is
-// too short for the pipeline idles only its own lane until its successor is ready; continued
-// and open chunks (streaming) still take the synchronous sha_setup path.
+// Per-lane mode: each lane hashes one chunk at a time, longest first within the address region
+// its wave works on (Regions). An iteration hashes BSG_LANE_BPI blocks per lane. Starting the
+// next job is pipelined per lane, one memory step per iteration, so no iteration waits for
+// more than what the one before issued:
+//   BSG_LANE_LEAD iterations before its job ends a lane pops a slot of its wave's region
+//   (one atomic per wave) -> loads the job id (rorder) -> loads its LaneJob (k_lens) -> in its
+//   last iteration prefetches the new job's first blocks instead of past-the-end ones and
+//   switches jobs in registers; the finished job's record is stored one iteration later.
+// The loop waits once per iteration, at its top, for everything the previous one issued (a
+// whole compression earlier). Round 2 first popped and set up the next job only when the last
+// one ended, and the whole wave waited for that atomic and ~4 dependent loads whenever any
+// lane switched. A job too short for the pipeline idles only its own lane until its successor
+// is ready; continued and open chunks (streaming) still take the synchronous sha_setup path.
 __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   constexpr int kBPI = BSG_LANE_BPI;  // blocks per iteration (per lane)
   const uint32_t lane = threadIdx.x & 63u;
@@ -1303,44 +1299,6 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   LANE_DIAG_END
 }
 
-#else  // BSG_LANE_PIPE == 0: round-2 form (experiment A/B)
-__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
-  const uint64_t nshort = a.ctr->nshort;
-  ShaJob jb;
-  uint32_t st[8];
-  RawBlock rb;
-  bool has = false, exhausted = false;
-  uint32_t blk = 0;
-  LANE_DIAG_INIT
-  for (;;) {
-    while (!has && !exhausted) {
-      const uint64_t q = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->job_head), 1ull);
-      if (q >= nshort) {
-        exhausted = true;
-      } else if (sha_setup(a, a.order[q], M, jb, st)) {
-        blk = 0;
-        if (jb.nblocks == 0) {
-          sha_finish(a, jb, st);
-        } else {
-          has = true;
-          if (jb.prefix == 0) raw_load(jb.dbase, 0, 0, jb.L, rb);
-        }
-      }
-    }
-    if (!has) break;
-    LANE_DIAG_ITER(true)
-    uint32_t W[16];
-    lane_words(jb, blk, rb, true, W);
-    raw_load(jb.dbase, 64ull * blk + 64, jb.prefix, jb.L, rb);
-    sha256_compress(st, W);
-    if (++blk == jb.nblocks) {
-      sha_finish(a, jb, st);
-      has = false;
-    }
-  }
-  LANE_DIAG_END
-}
-#endif
 
 // ---------------------------------------------------------------------------------------------
 // Wave-per-chunk path for the longest chunks. A SHA-256 chain is serial, so a batch's wall time
