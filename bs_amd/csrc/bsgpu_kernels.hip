@@ -1706,16 +1706,20 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   hs[2] = a_side ? st[2] : st[4];
   hs[3] = a_side ? st[3] : st[5];
 #endif
+  // Each ring fill's message block is requested one fill ahead, before the chain runs on the
+  // current fill, so a fill never waits for HBM (a pair ticket fills every 2 blocks).
+  RawBlock rb;
+  raw_load(ja.dbase, 64ull * min(lane % B, max(na, 1u) - 1u), 0, ja.L, rb);
   for (uint32_t base = 0; base < nmax; base += B) {
     // phase A: block base + lane % B of chain cA into LDS row `lane`; past a chain's last
     // block (or for an empty slot) the last block is re-expanded, so no load leaves the slack
     const uint32_t blk = min(base + lane % B, max(na, 1u) - 1u);
-    RawBlock rb;
-    raw_load(ja.dbase, 64ull * blk, 0, ja.L, rb);
     uint32_t W[16];
     raw_to_words(rb, W);
-    if (rb.valid < 64) {
-      pad_words(rb.valid, W);
+    const int32_t valid = rb.valid;
+    raw_load(ja.dbase, 64ull * min(base + B + lane % B, max(na, 1u) - 1u), 0, ja.L, rb);
+    if (valid < 64) {
+      pad_words(valid, W);
       if (ja.fin && blk + 1 == na) {
         const uint64_t bits = (ja.consumed + ja.L) * 8ull;
         W[14] = (uint32_t)(bits >> 32);
