@@ -335,7 +335,8 @@ struct bsg_engine {
                buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
                buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
                jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
-               rorder.as<uint64_t>(), data_span, long_mode(), 4u * (uint32_t)num_cus};
+               data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
+               long_mode(), 4u * (uint32_t)num_cus};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));

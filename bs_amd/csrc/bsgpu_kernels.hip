@@ -1377,7 +1377,8 @@ __global__ __launch_bounds__(256) void k_order(ShaArgs a) {
         a.long_list[h1[b] + rank] = j;
       } else {
         a.order[h0[b] + rank] = j;
-        a.oreg[h0[b] + rank] = (uint8_t)job_region(a, a.jdesc[j].dptr, (uint32_t)a.reg->nregions);
+        if (a.span > kRegionBytes)
+          a.oreg[h0[b] + rank] = (uint8_t)job_region(a, a.jdesc[j].dptr, (uint32_t)a.reg->nregions);
       }
     }
     __syncthreads();
@@ -1586,6 +1587,11 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
     const uint64_t rmax = min((uint64_t)kMaxRegions, max((uint64_t)a.waves / 16, (uint64_t)1));
     const uint64_t rspan = (a.span + kRegionBytes - 1) / kRegionBytes;
     a.reg->nregions = min(min(rmax, rspan), max((uint64_t)nshort / kMinRegionJobs, (uint64_t)1));
+    if (a.span <= kRegionBytes) {  // one region: the k_r* kernels are not launched, and
+      a.reg->off[0] = 0;           // per-lane mode reads the LPT order itself (rorder = order)
+      a.reg->off[1] = nshort;
+      a.reg->head[0] = 0;
+    }
     a.ctr->long_thresh = mx > (uint64_t)nlb * w ? mx - (uint64_t)nlb * w : 0;  // diagnostic
     a.ctr->nlong_grp = n8;
     a.ctr->tickets_grp = t8;
@@ -2033,10 +2039,12 @@ hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, 
   hipLaunchKernelGGL(k_order<false>, dim3(grid), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_order<true>, dim3(grid), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_rcount, dim3(kRegionSegs), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_rscan, dim3(kMaxRegions), dim3(kRegionSegs), 0, s, a);
-  hipLaunchKernelGGL(k_rtotal, dim3(1), dim3(kMaxRegions), 0, s, a);
-  hipLaunchKernelGGL(k_rscatter, dim3(kRegionSegs), dim3(256), 0, s, a);
+  if (a.span > kRegionBytes) {  // else one region (k_bucket_scan) over the LPT order itself
+    hipLaunchKernelGGL(k_rcount, dim3(kRegionSegs), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rscan, dim3(kMaxRegions), dim3(kRegionSegs), 0, s, a);
+    hipLaunchKernelGGL(k_rtotal, dim3(1), dim3(kMaxRegions), 0, s, a);
+    hipLaunchKernelGGL(k_rscatter, dim3(kRegionSegs), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 
