@@ -233,7 +233,13 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
                     "records in host memory; tile 256 MiB, 3 tiles in flight"}
 
 
-KERNEL_NAMES = {"k_scan": "bsg::k_scan(bsg::ScanArgs)", "k_sha": "bsg::k_sha(bsg::ShaArgs)"}
+# rocprofv3 names of each stage's kernels (k_sha: two instantiations launched back to back, one of
+# which returns at once; the stage's bytes are their sum)
+KERNEL_NAMES = {"k_scan": ("void bsg::k_scan<true>(bsg::ScanArgs)",
+                           "void bsg::k_scan<false>(bsg::ScanArgs)"),
+                "k_sha": ("void bsg::k_sha<true>(bsg::ShaArgs)",
+                          "void bsg::k_sha<false>(bsg::ShaArgs)",
+                          "bsg::k_sha(bsg::ShaArgs)")}  # (one kernel before the split)
 
 
 def pmc_traffic(kernel: str, workload: str):
@@ -241,7 +247,7 @@ def pmc_traffic(kernel: str, workload: str):
     (profiles/rNN_pmc.json, written by tools/pmc_summary.py from rocprofv3 FETCH_SIZE and
     WRITE_SIZE passes, gfx950 correction applied there). None if no summary matches."""
     import glob
-    full = KERNEL_NAMES.get(kernel)
+    names = KERNEL_NAMES.get(kernel, ())
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         try:
             with open(path) as f:
@@ -250,9 +256,10 @@ def pmc_traffic(kernel: str, workload: str):
             continue
         if not workload.startswith(doc.get("workload", "\0")):
             continue
-        k = doc.get("kernels", {}).get(full)
-        if k:
-            return int(k["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+        ks = [doc.get("kernels", {}).get(n) for n in names]
+        ks = [k for k in ks if k]
+        if ks:
+            return int(sum(k["hbm_bytes_per_launch"] for k in ks)), os.path.relpath(path, ROOT)
     return None, None
 
 

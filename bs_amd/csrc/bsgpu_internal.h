@@ -88,7 +88,7 @@ struct Params {
 struct Counters {
   uint64_t ncand;              // total candidates (from the strip-count scan)
   uint64_t nchunks;            // total boundaries = finalized chunks
-  uint64_t job_head;           // unused (round 1: the per-lane queue head; now Regions::head)
+  uint64_t help_wg;            // k_sha workgroups arrived (the first helped/2 run helped solo pairs)
   uint64_t overflow;           // candidate buffer too small (host grows and re-runs)
   uint64_t error;              // device-side sanity check failed (bug guard; run is invalid)
   uint64_t max_nblocks;        // longest SHA-256 job in blocks (k_lens)
@@ -109,7 +109,7 @@ struct Counters {
   uint64_t nlong_grp;          // long jobs on solo / kGroup tickets; the rest of the long list
   uint64_t tickets_grp;        //   runs on pair tickets (kPairGroup jobs, one lane pair each)
   uint64_t nrefine;            // strips k_scan listed for the exact pass (k_refine)
-  uint64_t pad_[1];
+  uint64_t helped;             // solo tickets [0, helped) run with a helper wave (k_sha)
 };
 static_assert(sizeof(Counters) == 256, "Counters layout");
 

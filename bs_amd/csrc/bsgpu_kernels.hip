@@ -40,6 +40,14 @@
 #ifndef BSG_PAIR_PCT
 #define BSG_PAIR_PCT 34
 #endif
+// Waves per k_sha workgroup (4; 8 is an experiment).
+#ifndef BSG_SHA_WAVES
+#define BSG_SHA_WAVES 4
+#endif
+// Solo tickets of lightly loaded launches run with a helper wave filling their rings (k_sha).
+#ifndef BSG_HELP_SOLO
+#define BSG_HELP_SOLO 1
+#endif
 // With the octet chains (round 2) a lightly loaded launch — all its blocks are less than a
 // tenth of what the chip's lanes hash while the longest chain runs — ends on the pair tickets
 // unless the group tier reaches further down: configs[1] 88.2 GiB/s at 56 %, 93.1 at 48 %
@@ -1595,6 +1603,12 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
     a.ctr->long_thresh = mx > (uint64_t)nlb * w ? mx - (uint64_t)nlb * w : 0;  // diagnostic
     a.ctr->nlong_grp = n8;
     a.ctr->tickets_grp = t8;
+    // lightly loaded: the solo tickets run with helper waves (k_sha<true>), the queue after them
+    const uint64_t helped = (BSG_HELP_SOLO && BSG_SHA_WAVES == 4 && light && a.long_mode == 0)
+                                ? min(min((uint64_t)n8, (uint64_t)kSolo), (uint64_t)a.waves / 2)
+                                : 0;
+    a.ctr->helped = helped;
+    a.ctr->long_head = helped;
     a.ctr->ntickets = t8 + (nlong - n8 + kPairGroup - 1) / kPairGroup;
   }
 }
@@ -1828,20 +1842,166 @@ __device__ __forceinline__ uint64_t pop_uniform(uint64_t* head) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Solo tickets of a lightly loaded launch, with a helper wave (BSG_HELP_SOLO). A solo chain's
+// wave otherwise stops every 64 blocks to expand the next 64 message schedules into its ring:
+// ~50 of its ~2,720 cycles per block, on the launch's critical path. Here the first workgroups
+// to start (k_sha<true>) take solo tickets in pairs: waves 0 and 1 run the two chains, waves 2
+// and 3 fill their rings, two halves of 64 K+W rows per chain, handed over by sequence numbers
+// in LDS (fill f goes to half f & 1; the filler publishes fill_seq = f / 2 + 1 after writing
+// its rows, the chain publishes done_seq = f / 2 + 1 after running them). The waves of a
+// workgroup are resident together, so the hand-off depends on nothing outside the workgroup;
+// every wait is bounded.
+constexpr uint32_t kHelpHalfWords = 64 * kLongRow;
+constexpr uint32_t kHelpOnes = 4 * kHelpHalfWords;     // the A lanes' row of ones
+constexpr uint32_t kHelpFlags = kHelpOnes + kLongRow;  // fill_seq[2][2], then done_seq[2][2]
+constexpr uint32_t kHelpWords = kHelpFlags + 8;
+constexpr uint32_t kHelpSlot = 4 * kRingWords;         // the workgroup's pair index (past all rings)
+
+__device__ __forceinline__ uint32_t lds_seq_load(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_seq_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // rows land first
+}
+// Waits until *p == want (wave-uniform). Bounded (~1 s); a timeout, never expected, flags a
+// device error so that the run fails instead of hanging.
+__device__ bool lds_seq_wait(const ShaArgs& a, uint32_t* p, uint32_t want) {
+  for (uint32_t i = 0; i < (1u << 24); ++i) {
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)lds_seq_load(p)) == want) return true;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if ((threadIdx.x & 63u) == 0)
+    atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 8ull);
+  return false;
+}
+
+// The chain wave of helped solo ticket t (the workgroup's chain c): sha_wave_job's octet loop
+// over the filler's halves.
+__device__ void sha_solo_chain(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t* lds,
+                               uint32_t c) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ShaJob jb;
+  uint32_t st[8];
+  const bool vb = sha_setup(a, a.long_list[t], M, jb, st);
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(vb ? jb.nblocks : 0u);  // one job: uniform
+  uint64_t tm0 = 0, tr0 = 0;
+  if (t == 0) {  // timing stamps of the longest job (read back as Counters::diag)
+    tm0 = __builtin_amdgcn_s_memtime();
+    tr0 = __builtin_amdgcn_s_memrealtime();
+  }
+  const OctLane ol = oct_lane();
+  uint32_t hs[4];
+  hs[0] = ol.a_side ? st[0] : st[6];
+  hs[1] = ol.a_side ? st[1] : st[7];
+  hs[2] = ol.a_side ? st[2] : st[4];
+  hs[3] = ol.a_side ? st[3] : st[5];
+  uint32_t* fill_seq = lds + kHelpFlags + 2 * c;
+  uint32_t* done_seq = lds + kHelpFlags + 4 + 2 * c;
+  const uint32_t* ones = lds + kHelpOnes;
+  uint32_t f = 0;
+  for (uint32_t base = 0; base < nb; base += 64, ++f) {
+    const uint32_t h = f & 1u;
+    if (!lds_seq_wait(a, fill_seq + h, f / 2 + 1)) return;
+    const uint32_t* krow = ol.a_side ? ones : lds + (2 * c + h) * kHelpHalfWords;
+    const uint32_t stride = ol.a_side ? 0u : 4u * kLongRow;
+    sha256_blocks_oct(hs, krow, stride, min(64u, nb - base), (int32_t)nb - (int32_t)base, ol);
+    if (lane == 0) lds_seq_store(done_seq + h, f / 2 + 1);
+  }
+  // H0..H3 from octet position 4 (an A lane), H4..H7 from position 0 (an E lane)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st[k] = (uint32_t)__shfl((int)hs[k], 4);
+  st[6] = (uint32_t)__shfl((int)hs[0], 0);
+  st[7] = (uint32_t)__shfl((int)hs[1], 0);
+  st[4] = (uint32_t)__shfl((int)hs[2], 0);
+  st[5] = (uint32_t)__shfl((int)hs[3], 0);
+  if (vb && lane == 0) {
+    sha_finish(a, jb, st);
+    if (t == 0) {
+      a.ctr->diag[1] = __builtin_amdgcn_s_memtime();
+      a.ctr->diag[3] = __builtin_amdgcn_s_memrealtime();
+      a.ctr->diag[0] = tm0;
+      a.ctr->diag[2] = tr0;
+      a.ctr->diag[4] = jb.nblocks;
+    }
+  }
+}
+
+// The filler wave of helped solo ticket t: fill f is the K+W rows of blocks 64f .. 64f+63
+// (lane l: block 64f + l, the last block again past the end), into half f & 1 once the chain
+// has run that half's previous fill. Each fill's block is requested one fill ahead.
+__device__ void sha_solo_fill(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t* lds,
+                              uint32_t c) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ShaJob ja;
+  uint32_t sta[8];
+  const bool va = sha_setup(a, a.long_list[t], M, ja, sta);
+  if (!va) {
+    ja.dbase = a.data;
+    ja.L = 0;
+    ja.fin = 0;
+    ja.consumed = 0;
+  }
+  const uint32_t na = __builtin_amdgcn_readfirstlane(va ? ja.nblocks : 0u);
+  uint32_t* fill_seq = lds + kHelpFlags + 2 * c;
+  uint32_t* done_seq = lds + kHelpFlags + 4 + 2 * c;
+  RawBlock rb;
+  raw_load(ja.dbase, 64ull * min(lane, max(na, 1u) - 1u), 0, ja.L, rb);
+  uint32_t f = 0;
+  for (uint32_t base = 0; base < na; base += 64, ++f) {
+    const uint32_t h = f & 1u;
+    if (f >= 2 && !lds_seq_wait(a, done_seq + h, f / 2)) return;
+    const uint32_t blk = min(base + lane, max(na, 1u) - 1u);
+    uint32_t W[16];
+    raw_to_words(rb, W);
+    const int32_t valid = rb.valid;
+    raw_load(ja.dbase, 64ull * min(base + 64u + lane, max(na, 1u) - 1u), 0, ja.L, rb);
+    if (valid < 64) {
+      pad_words(valid, W);
+      if (ja.fin && blk + 1 == na) {
+        const uint64_t bits = (ja.consumed + ja.L) * 8ull;
+        W[14] = (uint32_t)(bits >> 32);
+        W[15] = (uint32_t)bits;
+      }
+    }
+    u32x4a* row = reinterpret_cast<u32x4a*>(lds + (2 * c + h) * kHelpHalfWords + lane * kLongRow);
+#pragma unroll
+    for (int tt = 0; tt < 64; tt += 4) {
+      uint32_t kw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = tt + u;
+        if (i >= 16) {
+          const uint32_t w15 = W[(i - 15) & 15], w2 = W[(i - 2) & 15];
+          const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+          const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+          W[i & 15] = (W[i & 15] + s0) + (W[(i - 7) & 15] + s1);
+        }
+        kw[u] = kK256[i] + W[i & 15];
+      }
+      row[tt / 4] = u32x4a{kw[0], kw[1], kw[2], kw[3]};
+    }
+    if (lane == 0) lds_seq_store(fill_seq + h, f / 2 + 1);
+  }
+}
+
 // The SHA-256 kernel. One 256-thread workgroup per CU (its LDS request admits only one), so
 // each of the 4 waves owns a SIMD: one wave saturates a SIMD's integer VALU (~4.2 cycles per
 // wave-instruction; a second wave on the SIMD only runs in the first one's gaps), so stacking
 // waves gains nothing and would stall the latency-critical wave-mode chains. Every wave first
 // drains the long-job queue in wave mode, then turns to per-lane mode (longest-first order).
-#ifndef BSG_SHA_WAVES
-#define BSG_SHA_WAVES 4
-#endif
 constexpr uint32_t kShaWaves = BSG_SHA_WAVES;
 static_assert(kShaWaves == 4 || kShaWaves == 8, "4 chain-capable waves per workgroup (+4 lane-only)");
 
+// Two instantiations, launched back to back; the one that does not match the launch (helped
+// solo tickets or not, k_bucket_scan) returns at once. k_sha<false> holds no helper code, so
+// its per-lane loop keeps its register allocation: k_sha sits at the SGPR limit, and the
+// helper code in the same kernel made hipcc spill SGPRs inside that loop (configs[2] 880 ->
+// 760-840 GiB/s). k_sha<true> runs only lightly loaded launches, where per-lane mode is short.
+template <bool HELP>
 __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (a.ctr->overflow || a.ctr->error) return;
+  if ((a.ctr->helped != 0) != HELP) return;
   const uint64_t M = a.ctr->nchunks;
   if (M > a.chunk_cap) return;  // k_chunks flagged the error
   const uint64_t nlong = a.ctr->nlong;
@@ -1860,7 +2020,28 @@ __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
   if (kShaWaves > 4 && chain_wg && wv >= 4) return;
   uint32_t* ring = lds + (wv & 3u) * kRingWords;
   uint64_t t = ~0ull;
-  if (chain_wg) {
+  bool helper_wg = false;
+  if constexpr (HELP) {  // the first workgroups to start take the helped solo pairs
+    if (threadIdx.x == 0)
+      lds[kHelpSlot] = (uint32_t)atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->help_wg), 1ull);
+    __syncthreads();
+    const uint64_t helped = a.ctr->helped, hw = lds[kHelpSlot];
+    if (hw * 2 < helped) {  // workgroup-uniform
+      helper_wg = true;
+      for (uint32_t i = threadIdx.x; i < (uint32_t)kLongRow; i += blockDim.x) lds[kHelpOnes + i] = 1u;
+      if (threadIdx.x < 8) lds[kHelpFlags + threadIdx.x] = 0u;
+      __syncthreads();
+      const uint32_t c = wv & 1u;
+      const uint64_t ht = hw * 2 + c;
+      if (ht < helped) {
+        __builtin_amdgcn_s_setprio(3);
+        if (wv < 2) sha_solo_chain(a, M, ht, lds, c);
+        else sha_solo_fill(a, M, ht, lds, c);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  if (chain_wg && !helper_wg) {
     // row of ones after each wave's 64 K+W rows (the A lanes' kw in sha256_rounds_bank)
     for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 1u;
     // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
@@ -2025,10 +2206,13 @@ hipError_t launch_init(const InitArgs& a, hipStream_t s) {
 
 constexpr uint32_t kShaLds = 84 * 1024;  // > 80 KiB: one k_sha workgroup per CU (160 KiB LDS)
 static_assert(4 * kRingWords * 4 <= kShaLds, "wave rings fit");
+static_assert(kHelpWords <= kHelpSlot && (kHelpSlot + 1) * 4 <= kShaLds,
+              "helped solo rings and the pair slot fit");
 
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
   (void)job_bound;  // persistent: one workgroup per CU, waves loop over the job queues
-  hipLaunchKernelGGL(k_sha, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
+  hipLaunchKernelGGL(k_sha<true>, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
+  hipLaunchKernelGGL(k_sha<false>, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
   return hipGetLastError();
 }
 

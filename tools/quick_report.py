@@ -14,7 +14,7 @@ for q, nbytes in (("c1", 1 << 30), ("c2", 16 << 30)):
     p = os.path.join(O, f"q_{q}", "run_kernel_stats.csv")
     if os.path.exists(p):
         for r in csv.DictReader(open(p)):
-            if any(k in r["Name"] for k in ("k_scan", "k_refine", "k_sha(", "k_compact")):
+            if any(k in r["Name"] for k in ("k_scan", "k_refine", "k_sha", "k_compact")):
                 print(q, r["Name"][:40], round(float(r["AverageNs"]) / 1e3, 1), "us")
     p = os.path.join(O, f"qf_{q}", "run_counter_collection.csv")
     if os.path.exists(p):
