@@ -8,6 +8,8 @@ which the last chain would end under several schedules, from measured stage cost
 
   one batch (today)      every chain starts after the whole scan + selection
   G stream groups        group g is scanned g-th; its chains start after its own scan
+  P position phases      phase p scans every stream's p-th 1/P; the chains of the chunks that
+                         closed in it start after its selection
   position-major         all streams scanned front to back together; a chunk's chain starts
                          once the scan front has passed its end (its length is known)
 
@@ -86,6 +88,10 @@ def main() -> None:
         grp = s * G // args.streams
         end = (grp + 1) / G * args.scan_ms + args.sel_ms + nb * blk
         print(f"  {G:3d} stream groups scanned in turn         {end.max():.3f}")
+    for P in (2, 3, 4, 6, 8, 16):
+        ph = np.minimum(((o + ln - 1) * P) // L, P - 1)  # the phase in which the chunk closes
+        end = (ph + 1) / P * args.scan_ms + args.sel_ms + nb * blk
+        print(f"  {P:3d} position phases                      {end.max():.3f}")
     fr = (o + ln) / L * args.scan_ms + args.sel_ms + nb * blk
     print(f"  position-major, chain at its chunk's end {fr.max():.3f}")
 
