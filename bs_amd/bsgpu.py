@@ -83,6 +83,7 @@ def lib() -> ctypes.CDLL:
         "bsg_engine_destroy": (None, [vp]),
         "bsg_engine_run": (ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint32,
                                           ctypes.POINTER(Params)]),
+        "bsg_engine_hash": (ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint32]),
         "bsg_engine_finish": (ctypes.c_int, [vp, u64p]),
         "bsg_engine_chunks_device": (vp, [vp]),
         "bsg_engine_copy_chunks": (ctypes.c_int, [vp, vp, ctypes.c_uint64]),
@@ -97,6 +98,11 @@ def lib() -> ctypes.CDLL:
                                                 ctypes.POINTER(Params), u32p, vp,
                                                 ctypes.c_uint64, u64p, u64p]),
         "bsg_sha256_batch": (ctypes.c_int, [ctypes.c_int, vp, u64p, u64p, ctypes.c_uint32, vp]),
+        "bsg_hasher_new": (vp, [ctypes.c_int]),
+        "bsg_hasher_sum": (ctypes.c_int, [vp, vp, u64p, u64p, ctypes.c_uint32, vp]),
+        "bsg_hasher_sum_ptrs": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_void_p), u64p,
+                                               ctypes.c_uint32, vp]),
+        "bsg_hasher_free": (None, [vp]),
         "bsg_fill_splitmix": (ctypes.c_int, [ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64,
                                              vp]),
         "bsg_device_malloc": (vp, [ctypes.c_int, ctypes.c_size_t]),
@@ -220,6 +226,37 @@ def sha256_batch(blobs: list[bytes], device: int = 0) -> list[bytes]:
     return [refs[32 * i:32 * i + 32].tobytes() for i in range(len(arrs))]
 
 
+class Hasher:
+    """bsg_hasher: persistent batched SHA-256 (Blob.Ref of many blobs)."""
+
+    def __init__(self, device: int = 0):
+        self.h = lib().bsg_hasher_new(device)
+        if not self.h:
+            raise BsgError(-19, "bsg_hasher_new")
+
+    def sum_ptrs(self, blobs: list) -> list[bytes]:
+        """Scattered host blobs (bsg_hasher_sum_ptrs): one GPU call, no packing by the caller."""
+        keep = [np.frombuffer(bytes(b), dtype=np.uint8) if len(b) else np.zeros(1, np.uint8)
+                for b in blobs]
+        ptrs = (ctypes.c_void_p * max(len(keep), 1))(*[a.ctypes.data for a in keep])
+        lens = _u64([len(b) for b in blobs])
+        refs = np.zeros(32 * max(len(blobs), 1), dtype=np.uint8)
+        _check(lib().bsg_hasher_sum_ptrs(self.h, ptrs, _p(lens, ctypes.c_uint64), len(blobs),
+                                         refs.ctypes.data), "bsg_hasher_sum_ptrs")
+        return [refs[32 * i:32 * i + 32].tobytes() for i in range(len(blobs))]
+
+    def free(self):
+        if self.h:
+            lib().bsg_hasher_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 def fill_splitmix(ptr: int, nbytes: int, seed: int, stream: int | None = None,
                   device: int = 0) -> None:
     _check(lib().bsg_fill_splitmix(device, ptr, nbytes, seed, stream), "bsg_fill_splitmix")
@@ -281,6 +318,14 @@ class Engine:
         _check(lib().bsg_engine_run(self.h, d_ptr, _p(self._off, ctypes.c_uint64),
                                     _p(self._len, ctypes.c_uint64), self.nstreams,
                                     ctypes.byref(self._p)), "bsg_engine_run")
+
+    def hash(self, d_ptr: int, off, lens) -> None:
+        """bsg_engine_hash: SHA-256 of whole blobs (record i: blob i's ref), no splitting."""
+        self._off, self._len = _u64(off), _u64(lens)
+        self.nstreams = len(self._off)
+        _check(lib().bsg_engine_hash(self.h, d_ptr, _p(self._off, ctypes.c_uint64),
+                                     _p(self._len, ctypes.c_uint64), self.nstreams),
+               "bsg_engine_hash")
 
     def finish(self) -> int:
         n = ctypes.c_uint64(0)

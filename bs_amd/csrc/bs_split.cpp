@@ -35,17 +35,69 @@ std::string RefString(const Ref& r) {
   return s;
 }
 
-GpuHasher::~GpuHasher() { bsg_hasher_free(h_); }
+// GpuHashers take their bsg_hasher (device buffers, pinned staging, an engine) from a small
+// process-wide pool and give it back when destroyed, so a Reader or store created per file
+// does not set one up each time.
+namespace {
+std::mutex g_hasher_mu;
+std::vector<bsg_hasher*>& hasher_pool(int device) {
+  static auto* pools = new std::map<int, std::vector<bsg_hasher*>>();  // never destroyed
+  return (*pools)[device];
+}
+bsg_hasher* hasher_acquire(int device) {
+  {
+    std::lock_guard<std::mutex> g(g_hasher_mu);
+    auto& v = hasher_pool(device);
+    if (!v.empty()) {
+      bsg_hasher* h = v.back();
+      v.pop_back();
+      return h;
+    }
+  }
+  return bsg_hasher_new(device);
+}
+void hasher_release(int device, bsg_hasher* h) {
+  if (!h) return;
+  {
+    std::lock_guard<std::mutex> g(g_hasher_mu);
+    auto& v = hasher_pool(device);
+    if (v.size() < 4) {
+      v.push_back(h);
+      return;
+    }
+  }
+  bsg_hasher_free(h);
+}
+}  // namespace
+
+GpuHasher::~GpuHasher() { hasher_release(device_, h_); }
+
+Status Store::GetBlob(const Ref& ref, Blob* out) {
+  auto v = std::make_shared<std::vector<uint8_t>>();
+  Status s = Get(ref, v.get());
+  if (!s.ok()) return s;
+  out->size = v->size();
+  out->data = std::shared_ptr<const uint8_t>(v, v->data());
+  return Status::Ok();
+}
 
 Status GpuHasher::SumBatch(const uint8_t* base, const uint64_t* off, const uint64_t* len,
                            size_t n, Ref* refs) {
   if (n == 0) return Status::Ok();
   std::lock_guard<std::mutex> g(mu_);
-  if (!h_ && !(h_ = bsg_hasher_new(device_))) return Status::Err(BSG_EDEVICE, "bsg_hasher_new");
+  if (!h_ && !(h_ = hasher_acquire(device_))) return Status::Err(BSG_EDEVICE, "bsg_hasher_new");
   static const uint8_t empty = 0;
   static_assert(sizeof(Ref) == 32, "Ref is 32 packed bytes");
   int rc = bsg_hasher_sum(h_, base ? base : &empty, off, len, (uint32_t)n,
                           reinterpret_cast<uint8_t*>(refs));
+  return rc ? Status::Err(rc, std::string("sha256: ") + bsg_errstr(rc)) : Status::Ok();
+}
+
+Status GpuHasher::SumPtrs(const uint8_t* const* ptrs, const uint64_t* len, size_t n, Ref* refs) {
+  if (n == 0) return Status::Ok();
+  std::lock_guard<std::mutex> g(mu_);
+  if (!h_ && !(h_ = hasher_acquire(device_))) return Status::Err(BSG_EDEVICE, "bsg_hasher_new");
+  int rc = bsg_hasher_sum_ptrs(h_, ptrs, len, (uint32_t)n, reinterpret_cast<uint8_t*>(refs));
   return rc ? Status::Err(rc, std::string("sha256: ") + bsg_errstr(rc)) : Status::Ok();
 }
 
@@ -59,6 +111,14 @@ Status MemStore::Get(const Ref& ref, std::vector<uint8_t>* out) {
   auto it = blobs_.find(ref);
   if (it == blobs_.end()) return Status::Err(kNotFound, "not found");
   out->assign(it->second.bytes(), it->second.bytes() + it->second.size);
+  return Status::Ok();
+}
+
+Status MemStore::GetBlob(const Ref& ref, Blob* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blobs_.find(ref);
+  if (it == blobs_.end()) return Status::Err(kNotFound, "not found");
+  *out = it->second;
   return Status::Ok();
 }
 
@@ -617,34 +677,74 @@ std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err, bool
   r->g_ = g;
   r->verify_ = verify;
   r->device_ = device;
+  if (const char* e = std::getenv("BSG_VERIFY_WINDOW"))  // tests: small windows
+    r->window_bytes_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
   r->stack_.push_back(std::move(n));
   *err = Status::Ok();
   return r;
 }
 
-// Verify mode: one batched GPU SHA-256 over all chunks of the current leaf node.
-Status Reader::LoadLeaves() {
-  const std::vector<Child>& leaves = stack_.back().leaves;
-  cache_.assign(leaves.size(), {});
-  std::vector<uint64_t> off(leaves.size()), len(leaves.size());
-  uint64_t total = 0;
-  for (size_t k = 0; k < leaves.size(); ++k) {
-    Status s = g_->Get(leaves[k].ref, &cache_[k]);
-    if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
-    off[k] = total;
-    len[k] = cache_[k].size();
-    total += len[k];
+// Verify mode. The leaf nodes under `ref`, in order, until *total reaches the window size.
+Status Reader::CollectLeafNodes(const Ref& ref, uint64_t* total, std::vector<Node>* out) {
+  Node n;
+  Status s = get_node(g_, ref, &n);
+  if (!s.ok()) return Status::Err(s.code, "getting tree node: " + s.msg);
+  if (!n.leaves.empty()) {
+    *total += n.size;
+    out->push_back(std::move(n));
+    return Status::Ok();
   }
-  std::vector<uint8_t> packed(total ? total : 1);
-  for (size_t k = 0; k < leaves.size(); ++k)
-    if (len[k]) std::memcpy(packed.data() + off[k], cache_[k].data(), len[k]);
-  std::vector<uint8_t> refs(32 * leaves.size());
-  int rc = bsg_sha256_batch(device_, packed.data(), off.data(), len.data(),
-                            (uint32_t)leaves.size(), refs.data());
-  if (rc) return Status::Err(rc, std::string("verifying chunks: ") + bsg_errstr(rc));
-  for (size_t k = 0; k < leaves.size(); ++k)
-    if (std::memcmp(refs.data() + 32 * k, leaves[k].ref.data(), 32) != 0)
-      return Status::Err(kCorrupt, "chunk " + RefString(leaves[k].ref) + " fails verification");
+  for (const Child& c : n.nodes) {
+    if (*total >= window_bytes_) break;
+    if (!(s = CollectLeafNodes(c.ref, total, out)).ok()) return s;
+  }
+  return Status::Ok();
+}
+
+// Verify mode: fetch the chunks of stack_.back() (a leaf node) and of the leaf nodes after it,
+// up to kVerifyWindow bytes, check all of them in one batched GPU SHA-256 call (bsg_engine_hash
+// mode: the long chunks on wave-mode chains), and keep the verified copies: the current leaf's
+// in cache_, the others in window_ by leaf-node offset.
+Status Reader::VerifyWindow() {
+  window_.clear();
+  std::vector<Node> nodes;
+  nodes.push_back(stack_.back());
+  uint64_t total = stack_.back().size;
+  // the rest of the window in tree order: later siblings on each level of the path, bottom up
+  for (size_t lvl = stack_.size() - 1; lvl-- > 0 && total < window_bytes_;) {
+    const Node& parent = stack_[lvl];
+    const uint64_t on_path = stack_[lvl + 1].offset;
+    size_t c = 0;
+    while (c < parent.nodes.size() && parent.nodes[c].offset <= on_path) ++c;
+    for (; c < parent.nodes.size() && total < window_bytes_; ++c) {
+      Status s = CollectLeafNodes(parent.nodes[c].ref, &total, &nodes);
+      if (!s.ok()) return s;
+    }
+  }
+  std::vector<std::vector<Blob>> chunks(nodes.size());
+  std::vector<const uint8_t*> ptrs;
+  std::vector<uint64_t> lens;
+  std::vector<const Ref*> want;
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const std::vector<Child>& leaves = nodes[i].leaves;
+    chunks[i].resize(leaves.size());
+    for (size_t k = 0; k < leaves.size(); ++k) {
+      Status s = g_->GetBlob(leaves[k].ref, &chunks[i][k]);  // store/mem: no copy
+      if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
+      ptrs.push_back(chunks[i][k].bytes());
+      lens.push_back(chunks[i][k].size);
+      want.push_back(&leaves[k].ref);
+    }
+  }
+  if (!hasher_) hasher_.reset(new GpuHasher(device_));
+  std::vector<Ref> refs(ptrs.size());
+  Status s = hasher_->SumPtrs(ptrs.data(), lens.data(), ptrs.size(), refs.data());
+  if (!s.ok()) return Status::Err(s.code, "verifying chunks: " + s.msg);
+  for (size_t k = 0; k < refs.size(); ++k)
+    if (refs[k] != *want[k])
+      return Status::Err(kCorrupt, "chunk " + RefString(*want[k]) + " fails verification");
+  cache_ = std::move(chunks[0]);
+  for (size_t i = 1; i < nodes.size(); ++i) window_[nodes[i].offset] = std::move(chunks[i]);
   cache_valid_ = true;
   return Status::Ok();
 }
@@ -683,9 +783,16 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
       stack_.push_back(std::move(child));
       cache_valid_ = false;
     }
-    if (verify_ && !cache_valid_) {
-      Status s = LoadLeaves();
-      if (!s.ok()) return s;
+    if (verify_ && !cache_valid_) {  // the leaf node's chunks: from the window, else a new one
+      auto it = window_.find(stack_.back().offset);
+      if (it != window_.end() && it->second.size() == stack_.back().leaves.size()) {
+        cache_ = std::move(it->second);
+        window_.erase(it);
+        cache_valid_ = true;
+      } else {
+        Status s = VerifyWindow();
+        if (!s.ok()) return s;
+      }
     }
     const std::vector<Child>& leaves = stack_.back().leaves;
     size_t k = 0;
@@ -696,16 +803,17 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
         Status s = g_->Get(leaves[k].ref, &fetched);
         if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
       }
-      const std::vector<uint8_t>& chunk = verify_ ? cache_[k] : fetched;
+      const uint8_t* cdata = verify_ ? cache_[k].bytes() : fetched.data();
+      const size_t csize = verify_ ? cache_[k].size : fetched.size();
       // offsets come from store contents: check them before indexing (Go's bounds checks
       // would panic on the same trees)
-      if (leaves[k].offset > pos_ || pos_ - leaves[k].offset > chunk.size())
+      if (leaves[k].offset > pos_ || pos_ - leaves[k].offset > csize)
         return Status::Err(kCorrupt, "leaf offsets do not match chunk sizes");
       const uint64_t skip = pos_ - leaves[k].offset;
-      const size_t avail = chunk.size() - (size_t)skip;
+      const size_t avail = csize - (size_t)skip;
       if (avail == 0) return Status::Err(kCorrupt, "leaf offsets do not match chunk sizes");
       const size_t take = std::min(avail, len);
-      std::memcpy(buf, chunk.data() + skip, take);
+      std::memcpy(buf, cdata + skip, take);
       buf += take;
       len -= take;
       *got += take;

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -182,6 +183,7 @@ struct bsg_engine {
   uint64_t retry_cap = 0;  // exact candidate capacity after an overflow (one re-run)
   uint32_t nstreams = 0;
   bool enqueued = false;
+  bool hash_mode = false;  // bsg_engine_hash: every stream is one blob (enqueue_hash)
   Counters last{};
   // optional per-stage HIP events on the engine stream: [scan, compact..chunks, sha]
   bool profile = false;
@@ -345,6 +347,66 @@ struct bsg_engine {
     return BSG_OK;
   }
 
+  // bsg_engine_hash: every stream is one blob, hashed whole (Blob.Ref of many blobs): no scan or
+  // selection, one final chunk per stream, then the same job ordering and k_sha as a split run.
+  int enqueue_hash() {
+    const uint32_t ns = nstreams;
+    data_span = 1;
+    for (uint32_t s = 0; s < ns; ++s)
+      data_span = std::max<uint64_t>(data_span, descs[s].data_off + descs[s].len);
+    nstrips = 0;
+    cand_cap = 0;
+    chunk_cap = ns;
+    const uint64_t nn = ns ? ns : 1;
+    HCHECK(streams.ensure(sizeof(StreamDesc) * nn));
+    HCHECK(bnd_end.ensure(sizeof(uint64_t) * nn));
+    HCHECK(bnd_info.ensure(sizeof(uint64_t) * nn));
+    HCHECK(out.ensure(sizeof(ChunkRec) * nn));
+    HCHECK(scount.ensure(sizeof(uint64_t) * nn));
+    HCHECK(last_end.ensure(sizeof(uint64_t) * nn));
+    HCHECK(carry.ensure(sizeof(CarryOut) * nn));
+    HCHECK(ctr.ensure(sizeof(Counters)));
+    HCHECK(long_list.ensure(sizeof(uint64_t) * 2 * nn));
+    HCHECK(order.ensure(sizeof(uint64_t) * 2 * nn));
+    HCHECK(jinfo.ensure(sizeof(uint32_t) * 2 * nn));
+    HCHECK(jdesc.ensure(sizeof(LaneJob) * 2 * nn));
+    HCHECK(regions.ensure(sizeof(Regions)));
+    HCHECK(oreg.ensure(2 * nn));
+    HCHECK(rorder.ensure(sizeof(uint64_t) * 2 * nn));
+    HCHECK(buckets.ensure(sizeof(uint32_t) * 4 * kLptBuckets));
+    HCHECK(h_streams.ensure(sizeof(StreamDesc) * nn));
+    HCHECK(h_ctr.ensure(sizeof(Counters)));
+    std::memcpy(h_streams.p, descs.data(), sizeof(StreamDesc) * ns);
+    HCHECK(hipMemcpyAsync(streams.p, h_streams.p, sizeof(StreamDesc) * ns, hipMemcpyHostToDevice,
+                          stream));
+    HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
+    HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * 2 * kLptBuckets, stream));
+    Counters* dctr = ctr.as<Counters>();
+    InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
+                carry.as<CarryOut>()};
+    if (ns) HCHECK(dbg("launch_init", stream, launch_init(ia, stream)));
+    mark(0);
+    mark(1);  // no scan / selection stage
+    ChunkArgs ca{nullptr, nullptr, nullptr, bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(),
+                 scount.as<uint64_t>(), last_end.as<uint64_t>(), chunk_cap, p, dctr};
+    if (ns) HCHECK(dbg("launch_blob_jobs", stream,
+                       launch_blob_jobs(ca, streams.as<StreamDesc>(), ns, stream, num_cus)));
+    ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
+               bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
+               carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
+               buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
+               buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
+               jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
+               data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
+               long_mode(), 4u * (uint32_t)num_cus};
+    HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
+    mark(2);
+    HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
+    mark(3);
+    enqueued = true;
+    return BSG_OK;
+  }
+
   int finish(uint64_t* nchunks) {
     if (!enqueued) return BSG_ESTATE;
     for (int attempt = 0; attempt < 3; ++attempt) {
@@ -353,7 +415,7 @@ struct bsg_engine {
       last = *h_ctr.as<Counters>();
       if (!last.overflow) break;
       retry_cap = last.ncand + 1024;  // exact size for this input, then run again
-      int rc = enqueue();
+      int rc = hash_mode ? enqueue_hash() : enqueue();
       if (rc) return rc;
     }
     retry_cap = 0;
@@ -884,12 +946,12 @@ void bsg_engine_destroy(bsg_engine* e) {
   delete e;
 }
 
-int bsg_engine_run(bsg_engine* e, const uint8_t* d_data, const uint64_t* off, const uint64_t* len,
-                   uint32_t nstreams, const bsg_params* params) {
+// Checks a device-resident batch (16-byte aligned offsets, streams under 2^40 bytes, the read
+// slack inside the allocation) and fills the engine's descriptors: fresh, final streams.
+static int engine_batch(bsg_engine* e, const uint8_t* d_data, const uint64_t* off,
+                        const uint64_t* len, uint32_t nstreams) {
   if (!e || (nstreams && (!d_data || !off || !len)) || nstreams > 65535) return BSG_EINVAL;
-  Params p;
-  int rc = normalize(params, &p, nullptr);
-  if (rc) return rc;
+  int rc;
   if ((rc = e->setdev())) return rc;
   // the SHA-256 loader reads up to kReadSlack bytes past a stream's end (masked): that memory
   // must belong to the same allocation
@@ -925,8 +987,27 @@ int bsg_engine_run(bsg_engine* e, const uint8_t* d_data, const uint64_t* off, co
   }
   e->d_data = d_data;
   e->nstreams = nstreams;
+  return BSG_OK;
+}
+
+int bsg_engine_run(bsg_engine* e, const uint8_t* d_data, const uint64_t* off, const uint64_t* len,
+                   uint32_t nstreams, const bsg_params* params) {
+  Params p;
+  int rc = normalize(params, &p, nullptr);
+  if (rc) return rc;
+  if ((rc = engine_batch(e, d_data, off, len, nstreams))) return rc;
   e->p = p;
+  e->hash_mode = false;
   return e->enqueue();
+}
+
+int bsg_engine_hash(bsg_engine* e, const uint8_t* d_data, const uint64_t* off, const uint64_t* len,
+                    uint32_t nblobs) {
+  int rc = engine_batch(e, d_data, off, len, nblobs);
+  if (rc) return rc;
+  normalize(nullptr, &e->p, nullptr);
+  e->hash_mode = true;
+  return e->enqueue_hash();
 }
 
 int bsg_engine_finish(bsg_engine* e, uint64_t* nchunks) {
@@ -1219,12 +1300,91 @@ int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed
 // Batched Blob.Ref() with persistent device buffers and stream (bsg_hasher_*): a Writer hashes
 // every tree node through one, so a call costs one H2D, one launch and one D2H, not four
 // allocations.
+// Copies n blobs src[so[k] .. +sl[k]) to dst + dofs[k], on up to copy_threads() threads, each
+// taking a run of whole blobs of about total / threads bytes.
+static void par_gather(uint8_t* dst, const uint8_t* src, const uint64_t* so,
+                       const uint8_t* const* sp, const uint64_t* sl, const uint64_t* dofs,
+                       uint32_t n, uint64_t total) {
+  constexpr uint64_t kPiece = 2ull << 20;  // per thread, at least
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nt = (unsigned)std::min<uint64_t>({(uint64_t)copy_threads(), (uint64_t)hw,
+                                                    total / kPiece});
+  auto run = [=](uint32_t a, uint32_t b) {
+    for (uint32_t k = a; k < b; ++k)
+      if (sl[k]) std::memcpy(dst + dofs[k], sp ? sp[k] : src + so[k], sl[k]);
+  };
+  if (nt <= 1) {
+    run(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const uint64_t per = (total + nt - 1) / nt;
+  uint32_t a = 0;
+  uint64_t acc = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    acc += sl[k];
+    if (acc >= per || k + 1 == n) {
+      th.emplace_back(run, a, k + 1);
+      a = k + 1;
+      acc = 0;
+    }
+  }
+  for (auto& x : th) x.join();
+}
+
 struct bsg_hasher {
   int dev = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
   DevBuf data, off, len, refs;
   PinBuf h_meta;  // off[n] | len[n] staged for one H2D
+  // Large batches (the verifying split.Reader, bsg_sha256_batch of many blobs): the blobs are
+  // packed at 16-byte offsets into pinned staging and hashed by an engine in bsg_engine_hash
+  // mode, whose wave-mode chains take the longest blobs (k_sha_blobs hashes one blob per lane,
+  // so a batch waits for its longest blob at per-lane speed, ~2.5x slower per block).
+  static constexpr uint32_t kEngineMinBlobs = 16;
+  static constexpr uint64_t kEngineMinBytes = 4ull << 20;
+  static constexpr uint64_t kEngineBatch = 256ull << 20;  // bytes per engine run (one blob may exceed)
+  bsg_engine* eng = nullptr;
+  PinBuf stage;
+  DevBuf dstage;
+  std::vector<uint64_t> aoff;
+  std::vector<bsg_chunk> recs;
+
+  // blob k is base + o[k], or ptrs[k] when ptrs is given (scattered blobs, e.g. a store's)
+  int sum_engine(const uint8_t* base, const uint64_t* o, const uint8_t* const* ptrs,
+                 const uint64_t* l, uint32_t n, uint8_t* out) {
+    int err = 0;
+    if (!eng && !(eng = bsg_engine_create(dev, nullptr, &err))) return err ? err : BSG_EDEVICE;
+    hipStream_t es = static_cast<hipStream_t>(bsg_engine_stream(eng));
+    for (uint32_t i = 0; i < n;) {
+      uint64_t bytes = 0;
+      uint32_t j = i;
+      aoff.clear();
+      while (j < n && j - i < 65535u) {
+        const uint64_t a = (bytes + 15) & ~15ull;
+        if (j > i && a + l[j] > kEngineBatch) break;
+        aoff.push_back(a);
+        bytes = a + l[j];
+        ++j;
+      }
+      HCHECK(stage.ensure(bytes + kReadSlack));
+      HCHECK(dstage.ensure(bytes + kReadSlack));
+      par_gather(stage.as<uint8_t>(), base, o ? o + i : nullptr, ptrs ? ptrs + i : nullptr, l + i,
+                 aoff.data(), j - i, bytes);
+      if (bytes) HCHECK(hipMemcpyAsync(dstage.p, stage.p, bytes, hipMemcpyHostToDevice, es));
+      int rc = bsg_engine_hash(eng, dstage.as<uint8_t>(), aoff.data(), l + i, j - i);
+      uint64_t nch = 0;
+      if (!rc) rc = bsg_engine_finish(eng, &nch);
+      if (!rc && nch != j - i) rc = BSG_EDEVICE;
+      if (rc) return rc;
+      recs.resize(j - i);
+      if ((rc = bsg_engine_copy_chunks(eng, recs.data(), j - i))) return rc;
+      for (uint32_t k = 0; k < j - i; ++k) std::memcpy(out + 32ull * (i + k), recs[k].ref, 32);
+      i = j;
+    }
+    return BSG_OK;
+  }
 
   int sum(const uint8_t* base, const uint64_t* o, const uint64_t* l, uint32_t n, uint8_t* out) {
     hipPointerAttribute_t attr;
@@ -1233,8 +1393,13 @@ struct bsg_hasher {
       on_device = (attr.type == hipMemoryTypeDevice);
     else
       (void)hipGetLastError();
-    uint64_t hi = 0;
-    for (uint32_t i = 0; i < n; ++i) hi = std::max<uint64_t>(hi, o[i] + l[i]);
+    uint64_t hi = 0, total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      hi = std::max<uint64_t>(hi, o[i] + l[i]);
+      total += l[i];
+    }
+    if (!on_device && n >= kEngineMinBlobs && total >= kEngineMinBytes)
+      return sum_engine(base, o, nullptr, l, n, out);
     // always hash from a private copy with kReadSlack bytes of tail padding
     HCHECK(data.ensure(hi + kReadSlack));
     HCHECK(off.ensure(8ull * n));
@@ -1284,6 +1449,30 @@ int bsg_hasher_sum(bsg_hasher* h, const uint8_t* base, const uint64_t* off, cons
   return h->sum(base, off, len, n, refs);
 }
 
+int bsg_hasher_sum_ptrs(bsg_hasher* h, const uint8_t* const* ptrs, const uint64_t* len,
+                        uint32_t n, uint8_t* refs) {
+  if (!h || (n && (!ptrs || !len || !refs))) return BSG_EINVAL;
+  if (n == 0) return BSG_OK;
+  HCHECK(hipSetDevice(h->dev));
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (len[i] && !ptrs[i]) return BSG_EINVAL;
+    total += len[i];
+  }
+  if (n >= bsg_hasher::kEngineMinBlobs && total >= bsg_hasher::kEngineMinBytes)
+    return h->sum_engine(nullptr, nullptr, ptrs, len, n, refs);
+  // small batches: packed, then the one-blob-per-lane kernel
+  std::vector<uint8_t> packed(total ? total : 1);
+  std::vector<uint64_t> off(n);
+  uint64_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    off[i] = o;
+    if (len[i]) std::memcpy(packed.data() + o, ptrs[i], len[i]);
+    o += len[i];
+  }
+  return h->sum(packed.data(), off.data(), len, n, refs);
+}
+
 void bsg_hasher_free(bsg_hasher* h) {
   if (!h) return;
   hipSetDevice(h->dev);
@@ -1293,8 +1482,19 @@ void bsg_hasher_free(bsg_hasher* h) {
   h->len.release();
   h->refs.release();
   h->h_meta.release();
+  h->stage.release();
+  h->dstage.release();
+  if (h->eng) bsg_engine_destroy(h->eng);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
+}
+
+// bsg_sha256_batch keeps a few hashers (device buffers, pinned staging, an engine) for the next
+// call instead of creating and freeing them every time.
+static std::mutex g_hasher_pool_mu;
+static std::vector<bsg_hasher*>& hasher_pool() {
+  static auto* v = new std::vector<bsg_hasher*>();  // never destroyed (see ctx_pool)
+  return *v;
 }
 
 int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const uint64_t* len,
@@ -1302,10 +1502,31 @@ int bsg_sha256_batch(int device, const uint8_t* base, const uint64_t* off, const
   if (n && (!base || !off || !len || !refs)) return BSG_EINVAL;
   if (n == 0) return BSG_OK;
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
-  bsg_hasher* h = bsg_hasher_new(device);
-  if (!h) return BSG_EDEVICE;
+  bsg_hasher* h = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_hasher_pool_mu);
+    auto& v = hasher_pool();
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i]->dev == device) {
+        h = v[i];
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+  }
+  if (!h && !(h = bsg_hasher_new(device))) return BSG_EDEVICE;
+  if (hipSetDevice(device) != hipSuccess) {
+    bsg_hasher_free(h);
+    return BSG_EDEVICE;
+  }
   const int rc = h->sum(base, off, len, n, refs);
-  bsg_hasher_free(h);
+  {
+    std::lock_guard<std::mutex> g(g_hasher_pool_mu);
+    if (rc == BSG_OK && hasher_pool().size() < 2) {
+      hasher_pool().push_back(h);
+      h = nullptr;
+    }
+  }
+  if (h) bsg_hasher_free(h);
   return rc;
 }
 

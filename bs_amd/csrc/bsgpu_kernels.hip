@@ -718,6 +718,25 @@ __global__ __launch_bounds__(256) void k_tally(ChunkArgs a, uint32_t nstreams) {
   }
 }
 
+// bsg_engine_hash: every stream of the batch is one blob, hashed whole as one final chunk of
+// level 0 (no scan, no selection); k_lens / k_order / k_sha then run as for a split batch, so
+// the longest blobs get the wave-mode chains and the rest the per-lane LPT queues.
+__global__ __launch_bounds__(256) void k_blob_jobs(ChunkArgs a, const StreamDesc* streams,
+                                                   uint32_t nstreams) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nstreams;
+       s += gridDim.x * blockDim.x) {
+    const uint64_t L = streams[s].len;
+    a.bnd_end[s] = L;
+    a.bnd_info[s] = (uint64_t)s << 32;
+    a.scount[s] = 1;
+    a.last_end[s] = L;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.ctr->nchunks = nstreams;
+    a.ctr->ncand = nstreams;
+  }
+}
+
 __global__ void k_init(InitArgs a) {
   for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < a.nstreams;
        s += gridDim.x * blockDim.x) {
@@ -2196,6 +2215,13 @@ hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, uint32_t nstre
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tally, dim3(grid_for(nstreams, 256, 1024)), dim3(256), 0, s, a, nstreams);
+  return hipGetLastError();
+}
+
+hipError_t launch_blob_jobs(const ChunkArgs& a, const StreamDesc* streams, uint32_t nstreams,
+                            hipStream_t s, int num_cus) {
+  const uint32_t grid = grid_for(nstreams, 256, 4u * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_blob_jobs, dim3(grid), dim3(256), 0, s, a, streams, nstreams);
   return hipGetLastError();
 }
 

@@ -112,6 +112,8 @@ hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, i
 hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, uint32_t nstreams, hipStream_t s,
                          int num_cus);
 hipError_t launch_init(const InitArgs& a, hipStream_t s);
+hipError_t launch_blob_jobs(const ChunkArgs& a, const StreamDesc* streams, uint32_t nstreams,
+                            hipStream_t s, int num_cus);
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus);

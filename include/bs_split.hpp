@@ -46,10 +46,15 @@ constexpr int kNotFound = BSG_ENOTFOUND;  // bs.ErrNotFound (store.go:63)
 constexpr int kCorrupt = BSG_ECORRUPT;    // a fetched blob does not hash to its ref (Reader verify)
 constexpr int kIO = BSG_EIO;              // filesystem error (errno text in Status::msg)
 
+struct Blob;
+
 class Store {
  public:
   virtual ~Store() = default;
   virtual Status Get(const Ref& ref, std::vector<uint8_t>* out) = 0;
+  // Get with shared ownership of the bytes: a store holding blobs in memory hands out its own
+  // (store/mem), others read into a new buffer. The bytes never change afterwards.
+  virtual Status GetBlob(const Ref& ref, Blob* out);
   // Put adds the blob if absent; *ref = its SHA-256, *added = whether it was new.
   virtual Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) = 0;
   // Calls f for each ref > start in lexicographic order (store.go:21-23).
@@ -89,6 +94,8 @@ class GpuHasher {
   // refs[i] = SHA-256 of base[off[i] .. off[i] + len[i]) for n blobs, one GPU call.
   Status SumBatch(const uint8_t* base, const uint64_t* off, const uint64_t* len, size_t n,
                   Ref* refs);
+  // refs[i] = SHA-256 of ptrs[i][0 .. len[i]) (scattered blobs), one GPU call.
+  Status SumPtrs(const uint8_t* const* ptrs, const uint64_t* len, size_t n, Ref* refs);
 
  private:
   int device_;
@@ -100,6 +107,7 @@ class MemStore : public Store, public RefPutter {
  public:
   explicit MemStore(int device = 0) : hasher_(device) {}
   Status Get(const Ref& ref, std::vector<uint8_t>* out) override;
+  Status GetBlob(const Ref& ref, Blob* out) override;  // the stored Blob itself, no copy
   Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) override;
   Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
   Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
@@ -223,8 +231,9 @@ Status Protect(Store* g, const Ref& ref, std::vector<ProtectPair>* out);
 class Reader {
  public:
   // split.NewReader(ctx, g, ref). verify (not in the reference, which trusts its store): the
-  // leaves of each leaf node are fetched together and their SHA-256 checked against their refs
-  // in one batched GPU call (bsg_sha256_batch); a mismatch fails the Read with kCorrupt.
+  // chunks are fetched a window at a time (the leaf nodes from the one being read on, up to
+  // kVerifyWindow bytes) and their SHA-256 checked against their refs in one batched GPU call;
+  // reads are served from the verified copies, and a mismatch fails the Read with kCorrupt.
   static std::unique_ptr<Reader> New(Store* g, const Ref& root, Status* err,
                                      bool verify = false, int device = 0);
   // io.Reader: returns bytes read; 0 with *eof = true at the end.
@@ -235,14 +244,20 @@ class Reader {
 
  private:
   Reader() = default;
-  Status LoadLeaves();  // verify mode: fetch + check every leaf of stack_.back()
+  static constexpr uint64_t kVerifyWindow = 256ull << 20;  // bytes verified per GPU call
+  uint64_t window_bytes_ = kVerifyWindow;                 // (BSG_VERIFY_WINDOW overrides)
+  Status VerifyWindow();  // verify mode: fetch + check the leaf nodes from stack_.back() on
+  Status CollectLeafNodes(const Ref& ref, uint64_t* total, std::vector<Node>* out);
   Store* g_ = nullptr;
   uint64_t pos_ = 0;
   std::vector<Node> stack_;  // stack_[0] is the root
   bool verify_ = false;
   int device_ = 0;
-  bool cache_valid_ = false;                 // cache_ holds stack_.back()'s leaves
-  std::vector<std::vector<uint8_t>> cache_;  // verified chunks of that leaf node
+  bool cache_valid_ = false;  // cache_ holds stack_.back()'s leaves
+  std::vector<Blob> cache_;   // verified chunks of that leaf node
+  // verified chunks of the window's later leaf nodes, by leaf-node offset
+  std::map<uint64_t, std::vector<Blob>> window_;
+  std::unique_ptr<GpuHasher> hasher_;
 };
 
 }  // namespace split

@@ -118,6 +118,13 @@ void bsg_engine_destroy(bsg_engine* eng);
 #define BSG_READ_SLACK 256
 int bsg_engine_run(bsg_engine* eng, const uint8_t* d_data, const uint64_t* off,
                    const uint64_t* len, uint32_t nstreams, const bsg_params* params);
+/* Enqueue SHA-256 of nblobs whole blobs d_data[off[i] .. off[i]+len[i]) (bs.Blob.Ref,
+ * bs.go:24-26, for many blobs at once: the read-side verification of split.Reader, a store's
+ * batched Puts): same constraints as bsg_engine_run (device memory, off[i] % 16 == 0, at most
+ * 65,535 blobs, BSG_READ_SLACK readable bytes after the last); no splitting, record i (after
+ * bsg_engine_finish) carries blob i's ref, offset 0 and len[i]. Asynchronous. */
+int bsg_engine_hash(bsg_engine* eng, const uint8_t* d_data, const uint64_t* off,
+                    const uint64_t* len, uint32_t nblobs);
 /* Wait for the run; handles candidate-buffer growth (re-runs once if needed). Returns the
  * total chunk count in *nchunks. */
 int bsg_engine_finish(bsg_engine* eng, uint64_t* nchunks);
@@ -162,6 +169,11 @@ typedef struct bsg_hasher bsg_hasher;
 bsg_hasher* bsg_hasher_new(int device);
 int bsg_hasher_sum(bsg_hasher* h, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                    uint32_t n, uint8_t* refs);
+/* The same for scattered blobs: blob i is ptrs[i][0 .. len[i]) (host memory), e.g. the chunks a
+ * store holds separately. Large batches (>= 16 blobs and 4 MiB) are packed into pinned staging
+ * and hashed in bsg_engine_hash mode; small ones by one blob per lane. */
+int bsg_hasher_sum_ptrs(bsg_hasher* h, const uint8_t* const* ptrs, const uint64_t* len,
+                        uint32_t n, uint8_t* refs);
 void bsg_hasher_free(bsg_hasher* h);
 
 /* Device memory helpers (so callers need no second HIP runtime): kind 0 = H2D, 1 = D2H,

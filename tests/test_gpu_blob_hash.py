@@ -1,0 +1,130 @@
+"""Batched Blob.Ref (bs.go:24-26) of many blobs through the engine's hash mode (bsg_engine_hash,
+bsg_hasher_sum / _ptrs, bsg_sha256_batch), and the verifying split.Reader that uses it a window
+of leaf nodes at a time. Every ref is compared with hashlib (FIPS 180-4)."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _blobs(seed: int, n: int, mean: int):
+    rng = np.random.default_rng(seed)
+    lens = rng.exponential(mean, n).astype(np.int64)
+    # SHA-256 padding edges, empty blobs and a few long ones
+    edge = [0, 0, 1, 55, 56, 63, 64, 65, 119, 120, 127, 128, 4095, 4096, 1 << 20, 3 << 20]
+    k = min(n, len(edge))
+    lens[:k] = edge[:k]
+    rng.shuffle(lens)
+    data = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8).tobytes()
+    out, o = [], 0
+    for ln in lens:
+        out.append(data[o:o + int(ln)])
+        o += int(ln)
+    return out
+
+
+def test_sha256_batch_engine_path(gpu):
+    blobs = _blobs(5, 2000, 50_000)  # >= 16 blobs and 4 MiB: packed, bsg_engine_hash mode
+    assert sum(map(len, blobs)) > 64 << 20
+    got = gpu.sha256_batch(blobs)
+    assert got == [hashlib.sha256(b).digest() for b in blobs]
+
+
+def test_hasher_sum_ptrs_engine_and_small(gpu):
+    h = gpu.Hasher()
+    try:
+        big = _blobs(6, 600, 40_000)
+        assert h.sum_ptrs(big) == [hashlib.sha256(b).digest() for b in big]
+        small = _blobs(7, 9, 100)  # below the engine threshold: one blob per lane
+        small[0] = b""
+        assert h.sum_ptrs(small) == [hashlib.sha256(b).digest() for b in small]
+        assert h.sum_ptrs(big[:300]) == [hashlib.sha256(b).digest() for b in big[:300]]  # reuse
+    finally:
+        h.free()
+
+
+def test_sha256_batch_over_65535_blobs(gpu):
+    rng = np.random.default_rng(8)
+    lens = rng.integers(0, 160, 70_000)
+    lens[::997] = 40_000  # 4 MiB in all, so the engine path splits into two runs
+    data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8).tobytes()
+    blobs, o = [], 0
+    for ln in lens:
+        blobs.append(data[o:o + int(ln)])
+        o += int(ln)
+    assert sum(map(len, blobs)) >= 4 << 20
+    assert gpu.sha256_batch(blobs) == [hashlib.sha256(b).digest() for b in blobs]
+
+
+def test_engine_hash_device_resident(gpu):
+    blobs = _blobs(9, 300, 30_000)
+    off, o = [], 0
+    for b in blobs:
+        off.append(o)
+        o = (o + len(b) + 15) & ~15
+    host = np.zeros(o + gpu.READ_SLACK, dtype=np.uint8)
+    for b, x in zip(blobs, off):
+        host[x:x + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    buf = gpu.DeviceBuffer(host.size)
+    eng = gpu.Engine()
+    try:
+        buf.from_host(host)
+        eng.hash(buf.ptr, off, [len(b) for b in blobs])
+        assert eng.finish() == len(blobs)
+        ch = eng.chunks()
+        assert [bytes(r) for r in ch["ref"]] == [hashlib.sha256(b).digest() for b in blobs]
+        assert list(ch["len"]) == [len(b) for b in blobs]
+        assert list(ch["stream"]) == list(range(len(blobs)))
+    finally:
+        eng.close()
+        buf.free()
+
+
+@pytest.fixture
+def small_windows(monkeypatch):
+    monkeypatch.setenv("BSG_VERIFY_WINDOW", "65536")
+
+
+def test_reader_verify_windows(gpu, small_windows, tmp_path):
+    """Windows of 64 KiB over a tree with many small leaf nodes on several levels (Bits 10,
+    Fanout 2): every read and seek returns the stream's bytes; a corrupted chunk far from the
+    read position is caught when its window is verified."""
+    from bs_amd.synth import splitmix_bytes
+    data = splitmix_bytes(41, 6_000_000)
+    fs = gpu.FileStore(str(tmp_path))
+    w = gpu.Writer(fs, bits=10, min_size=64, fanout=2)
+    for i in range(0, len(data), 1 << 20):
+        w.write(data[i:i + (1 << 20)])
+    w.close()
+    root = w.root
+    w.free()
+    assert gpu.Reader(fs, root, verify=True).read_all() == data
+    r = gpu.Reader(fs, root, verify=True)
+    rng = np.random.default_rng(3)
+    for _ in range(40):
+        pos = int(rng.integers(0, len(data)))
+        n = int(rng.integers(1, 300_000))
+        assert r.seek(pos, 0) == pos
+        assert r.read(n) == data[pos:pos + n]
+    # corrupt one chunk in the last quarter of the stream
+    victim = None
+    for ref in fs.refs():
+        b = fs.get(ref)
+        k = data.find(b)
+        if len(b) > 200 and k > len(data) * 3 // 4:
+            victim = ref
+            break
+    assert victim is not None
+    p = os.path.join(str(tmp_path), "blobs", victim.hex()[:2], victim.hex()[:4], victim.hex())
+    with open(p, "r+b") as f:
+        c = f.read(1)
+        f.seek(0)
+        f.write(bytes([c[0] ^ 0x5A]))
+    r = gpu.Reader(fs, root, verify=True)
+    assert r.read(1 << 20) == data[: 1 << 20]  # the first windows are intact
+    with pytest.raises(gpu.BsgError) as ei:
+        r.read_all()
+    assert ei.value.code == gpu.CORRUPT
