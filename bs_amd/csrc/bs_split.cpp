@@ -684,43 +684,60 @@ std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err, bool
   return r;
 }
 
-// Verify mode. The leaf nodes under `ref`, in order, until *total reaches the window size.
-Status Reader::CollectLeafNodes(const Ref& ref, uint64_t* total, std::vector<Node>* out) {
-  Node n;
-  Status s = get_node(g_, ref, &n);
-  if (!s.ok()) return Status::Err(s.code, "getting tree node: " + s.msg);
-  if (!n.leaves.empty()) {
-    *total += n.size;
-    out->push_back(std::move(n));
-    return Status::Ok();
+Reader::~Reader() {
+  if (ahead_.valid()) ahead_.wait();  // the background window uses this Reader's store, hasher
+}
+
+// Verify mode. The next leaf node of the walk `cur` (a node with leaves), fetching the internal
+// nodes on the way; *done at the end of the tree.
+Status Reader::NextLeafNode(std::vector<Frame>* cur, Node* out, bool* done) {
+  *done = false;
+  while (!cur->empty()) {
+    Frame& f = cur->back();
+    if (f.next >= f.node.nodes.size()) {
+      cur->pop_back();
+      continue;
+    }
+    const Ref ref = f.node.nodes[f.next++].ref;
+    Node n;
+    Status s = get_node(g_, ref, &n);
+    if (!s.ok()) return Status::Err(s.code, "getting tree node: " + s.msg);
+    if (!n.leaves.empty()) {
+      *out = std::move(n);
+      return Status::Ok();
+    }
+    cur->push_back(Frame{std::move(n), 0});
   }
-  for (const Child& c : n.nodes) {
-    if (*total >= window_bytes_) break;
-    if (!(s = CollectLeafNodes(c.ref, total, out)).ok()) return s;
-  }
+  *done = true;
   return Status::Ok();
 }
 
-// Verify mode: fetch the chunks of stack_.back() (a leaf node) and of the leaf nodes after it,
-// up to kVerifyWindow bytes, check all of them in one batched GPU SHA-256 call (bsg_engine_hash
-// mode: the long chunks on wave-mode chains), and keep the verified copies: the current leaf's
-// in cache_, the others in window_ by leaf-node offset.
-Status Reader::VerifyWindow() {
-  window_.clear();
+// Verify mode: `first` (if given) and the leaf nodes after it in the walk, up to `budget` bytes:
+// their chunks fetched through Store::GetBlob (store/mem hands out its own Blobs, no copy) and
+// checked in one batched GPU SHA-256 call (bsg_hasher_sum_ptrs: bsg_engine_hash mode, the
+// long chunks on wave-mode chains). Runs on the reading thread or on the background one.
+Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint64_t budget) {
+  Window w;
   std::vector<Node> nodes;
-  nodes.push_back(stack_.back());
-  uint64_t total = stack_.back().size;
-  // the rest of the window in tree order: later siblings on each level of the path, bottom up
-  for (size_t lvl = stack_.size() - 1; lvl-- > 0 && total < window_bytes_;) {
-    const Node& parent = stack_[lvl];
-    const uint64_t on_path = stack_[lvl + 1].offset;
-    size_t c = 0;
-    while (c < parent.nodes.size() && parent.nodes[c].offset <= on_path) ++c;
-    for (; c < parent.nodes.size() && total < window_bytes_; ++c) {
-      Status s = CollectLeafNodes(parent.nodes[c].ref, &total, &nodes);
-      if (!s.ok()) return s;
-    }
+  uint64_t total = 0;
+  if (first) {
+    nodes.push_back(*first);
+    total = first->size;
   }
+  while (total < budget) {
+    Node n;
+    bool done = false;
+    w.st = NextLeafNode(&cur, &n, &done);
+    if (!w.st.ok()) return w;
+    if (done) {
+      w.end = true;
+      break;
+    }
+    total += n.size;
+    nodes.push_back(std::move(n));
+  }
+  w.cursor = std::move(cur);
+  for (const Node& n : nodes) w.covered.push_back(n.offset);
   std::vector<std::vector<Blob>> chunks(nodes.size());
   std::vector<const uint8_t*> ptrs;
   std::vector<uint64_t> lens;
@@ -729,22 +746,80 @@ Status Reader::VerifyWindow() {
     const std::vector<Child>& leaves = nodes[i].leaves;
     chunks[i].resize(leaves.size());
     for (size_t k = 0; k < leaves.size(); ++k) {
-      Status s = g_->GetBlob(leaves[k].ref, &chunks[i][k]);  // store/mem: no copy
-      if (!s.ok()) return Status::Err(s.code, "getting chunk: " + s.msg);
+      Status s = g_->GetBlob(leaves[k].ref, &chunks[i][k]);
+      if (!s.ok()) {
+        w.st = Status::Err(s.code, "getting chunk: " + s.msg);
+        return w;
+      }
       ptrs.push_back(chunks[i][k].bytes());
       lens.push_back(chunks[i][k].size);
       want.push_back(&leaves[k].ref);
     }
   }
-  if (!hasher_) hasher_.reset(new GpuHasher(device_));
   std::vector<Ref> refs(ptrs.size());
   Status s = hasher_->SumPtrs(ptrs.data(), lens.data(), ptrs.size(), refs.data());
-  if (!s.ok()) return Status::Err(s.code, "verifying chunks: " + s.msg);
+  if (!s.ok()) {
+    w.st = Status::Err(s.code, "verifying chunks: " + s.msg);
+    return w;
+  }
   for (size_t k = 0; k < refs.size(); ++k)
-    if (refs[k] != *want[k])
-      return Status::Err(kCorrupt, "chunk " + RefString(*want[k]) + " fails verification");
-  cache_ = std::move(chunks[0]);
-  for (size_t i = 1; i < nodes.size(); ++i) window_[nodes[i].offset] = std::move(chunks[i]);
+    if (refs[k] != *want[k]) {
+      w.st = Status::Err(kCorrupt, "chunk " + RefString(*want[k]) + " fails verification");
+      return w;
+    }
+  for (size_t i = 0; i < nodes.size(); ++i) w.leaves[nodes[i].offset] = std::move(chunks[i]);
+  return w;
+}
+
+// Verify mode: cache_ = the verified chunks of stack_.back(). From the current window if it
+// holds them; else from the window verified in the background, if it does; else a window is
+// verified here, starting at this leaf node (the first read, or after a seek). Each time a
+// window is taken, the one after it is started in the background.
+Status Reader::TakeLeaf() {
+  const uint64_t at = stack_.back().offset;
+  auto take = [&](Window&& w) -> Status {
+    if (!w.st.ok()) {
+      window_.clear();
+      if (std::find(w.covered.begin(), w.covered.end(), at) != w.covered.end()) return w.st;
+      return Status::Ok();  // a failure further on, in a window this read does not need
+    }
+    window_ = std::move(w.leaves);
+    if (!w.end)
+      ahead_ = std::async(std::launch::async,
+                          [this, cur = std::move(w.cursor)]() mutable {
+                            return VerifyRun(std::move(cur), nullptr, window_bytes_);
+                          });
+    return Status::Ok();
+  };
+  auto it = window_.find(at);
+  if (it == window_.end() && ahead_.valid()) {
+    Status s = take(ahead_.get());
+    if (!s.ok()) return s;
+    it = window_.find(at);
+  }
+  if (it == window_.end()) {
+    if (ahead_.valid()) ahead_.wait();  // a window for elsewhere in the stream: dropped
+    ahead_ = std::future<Window>();
+    if (!hasher_) hasher_.reset(new GpuHasher(device_));
+    // the walk, positioned after stack_.back(): each internal node on the path and its child
+    // after the one on the path
+    std::vector<Frame> cur;
+    for (size_t lvl = 0; lvl + 1 < stack_.size(); ++lvl) {
+      const Node& parent = stack_[lvl];
+      const uint64_t on_path = stack_[lvl + 1].offset;
+      size_t c = 0;
+      while (c < parent.nodes.size() && parent.nodes[c].offset <= on_path) ++c;
+      cur.push_back(Frame{parent, c});
+    }
+    Window w = VerifyRun(std::move(cur), &stack_.back(), window_bytes_);
+    if (!w.st.ok()) return w.st;
+    Status s = take(std::move(w));
+    if (!s.ok()) return s;
+    it = window_.find(at);
+    if (it == window_.end()) return Status::Err(kCorrupt, "tree node offsets repeat");
+  }
+  cache_ = std::move(it->second);
+  window_.erase(it);
   cache_valid_ = true;
   return Status::Ok();
 }
@@ -783,16 +858,11 @@ Status Reader::Read(uint8_t* buf, size_t len, size_t* got, bool* eof) {
       stack_.push_back(std::move(child));
       cache_valid_ = false;
     }
-    if (verify_ && !cache_valid_) {  // the leaf node's chunks: from the window, else a new one
-      auto it = window_.find(stack_.back().offset);
-      if (it != window_.end() && it->second.size() == stack_.back().leaves.size()) {
-        cache_ = std::move(it->second);
-        window_.erase(it);
-        cache_valid_ = true;
-      } else {
-        Status s = VerifyWindow();
-        if (!s.ok()) return s;
-      }
+    if (verify_ && !cache_valid_) {
+      Status s = TakeLeaf();
+      if (!s.ok()) return s;
+      if (cache_.size() != stack_.back().leaves.size())
+        return Status::Err(kCorrupt, "tree node offsets repeat");
     }
     const std::vector<Child>& leaves = stack_.back().leaves;
     size_t k = 0;

@@ -19,6 +19,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -246,8 +247,23 @@ class Reader {
   Reader() = default;
   static constexpr uint64_t kVerifyWindow = 256ull << 20;  // bytes verified per GPU call
   uint64_t window_bytes_ = kVerifyWindow;                 // (BSG_VERIFY_WINDOW overrides)
-  Status VerifyWindow();  // verify mode: fetch + check the leaf nodes from stack_.back() on
-  Status CollectLeafNodes(const Ref& ref, uint64_t* total, std::vector<Node>* out);
+  // Verify mode. A resumable walk over the tree's leaf nodes in order (one frame per internal
+  // node on the path: the node and its next child), and a window: the verified chunks of a run
+  // of leaf nodes, by leaf-node offset, with the walk positioned after them.
+  struct Frame {
+    Node node;
+    size_t next = 0;
+  };
+  struct Window {
+    std::map<uint64_t, std::vector<Blob>> leaves;
+    std::vector<Frame> cursor;
+    std::vector<uint64_t> covered;  // its leaf-node offsets (also when verification failed)
+    Status st;
+    bool end = false;               // the walk reached the last leaf node
+  };
+  Status NextLeafNode(std::vector<Frame>* cur, Node* out, bool* done);
+  Window VerifyRun(std::vector<Frame> cur, const Node* first, uint64_t budget);
+  Status TakeLeaf();  // cache_ = the verified chunks of stack_.back()
   Store* g_ = nullptr;
   uint64_t pos_ = 0;
   std::vector<Node> stack_;  // stack_[0] is the root
@@ -258,6 +274,11 @@ class Reader {
   // verified chunks of the window's later leaf nodes, by leaf-node offset
   std::map<uint64_t, std::vector<Blob>> window_;
   std::unique_ptr<GpuHasher> hasher_;
+  // the next window, fetched and verified on a background thread while this one is read
+  std::future<Window> ahead_;
+
+ public:
+  ~Reader();
 };
 
 }  // namespace split
