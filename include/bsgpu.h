@@ -226,8 +226,10 @@ void bsg_writer_free(bsg_writer* w);
 
 typedef struct bsg_reader bsg_reader; /* split.NewReader / Read / Seek / Size */
 bsg_reader* bsg_reader_new(bsg_store* s, const uint8_t root[32], int* err);
-/* flags: BSG_READER_VERIFY = check every fetched chunk's SHA-256 against its ref, one batched
- * GPU call per leaf node (a mismatch fails the read with BSG_ECORRUPT). */
+/* flags: BSG_READER_VERIFY = check every fetched chunk's SHA-256 against its ref: a window of
+ * leaf nodes (up to 256 MiB; BSG_VERIFY_WINDOW bytes if set) per batched GPU call, the next
+ * window verified in the background while this one is read; a read that needs a chunk of a
+ * window that failed returns BSG_ECORRUPT. */
 #define BSG_READER_VERIFY 1
 bsg_reader* bsg_reader_open(bsg_store* s, const uint8_t root[32], int flags, int device,
                             int* err);
