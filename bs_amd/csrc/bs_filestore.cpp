@@ -89,7 +89,100 @@ std::string FileStore::BlobPath(const Ref& ref) const {  // file.go:33-40
   return root_ + "/blobs/" + h.substr(0, 2) + "/" + h.substr(0, 4) + "/" + h;
 }
 
+FileStore::~FileStore() {
+  (void)Flush();
+  {
+    std::lock_guard<std::mutex> g(wb_mu_);
+    wb_stop_ = true;
+  }
+  wb_cv_.notify_all();
+  for (std::thread& t : wb_threads_) t.join();
+}
+
+Status FileStore::MkdirFor(const std::string& path) {
+  const std::string dir = path.substr(0, path.find_last_of('/'));
+  const std::string hhhh = dir.substr(dir.size() - 4);
+  uint32_t k = 0;
+  for (char c : hhhh) k = k << 4 | (uint32_t)(c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10);
+  {
+    std::lock_guard<std::mutex> g(dir_mu_);
+    if (dirs_made_[k & 0xffff]) return Status::Ok();
+  }
+  Status s = mkdir_all(dir);
+  if (!s.ok()) return s;
+  std::lock_guard<std::mutex> g(dir_mu_);
+  dirs_made_[k & 0xffff] = true;
+  return Status::Ok();
+}
+
+Status FileStore::PutBlob(const Ref& ref, const Blob& b, bool* added) {
+  std::unique_lock<std::mutex> g(wb_mu_);
+  if (!wb_err_.ok()) return wb_err_;
+  if (added) *added = false;
+  if (wb_pending_.count(ref)) return Status::Ok();
+  if (wb_threads_.empty())
+    for (int i = 0; i < kWriterThreads; ++i) wb_threads_.emplace_back([this] { Worker(); });
+  // bounded: wait for the writers when a GiB is pending
+  wb_done_cv_.wait(g, [&] { return wb_bytes_ < kWriteBehindBytes || !wb_err_.ok(); });
+  if (!wb_err_.ok()) return wb_err_;
+  wb_pending_.emplace(ref, b);
+  wb_bytes_ += b.size;
+  wb_queue_.emplace_back(ref, b);
+  if (added) *added = true;
+  g.unlock();
+  wb_cv_.notify_one();
+  return Status::Ok();
+}
+
+void FileStore::Worker() {
+  for (;;) {
+    std::pair<Ref, Blob> job;
+    {
+      std::unique_lock<std::mutex> g(wb_mu_);
+      wb_cv_.wait(g, [&] { return wb_stop_ || !wb_queue_.empty(); });
+      if (wb_queue_.empty()) return;  // stopping
+      job = std::move(wb_queue_.front());
+      wb_queue_.pop_front();
+    }
+    bool added = false;
+    Status s = PutWithRef(job.first, job.second.bytes(), job.second.size, &added);
+    {
+      std::lock_guard<std::mutex> g(wb_mu_);
+      if (!s.ok() && wb_err_.ok()) wb_err_ = s;
+      wb_pending_.erase(job.first);
+      wb_bytes_ -= job.second.size;
+    }
+    wb_done_cv_.notify_all();
+  }
+}
+
+Status FileStore::Flush() {
+  std::unique_lock<std::mutex> g(wb_mu_);
+  wb_done_cv_.wait(g, [&] { return wb_pending_.empty(); });
+  return wb_err_;
+}
+
+Status FileStore::GetBlob(const Ref& ref, Blob* out) {
+  {
+    std::lock_guard<std::mutex> g(wb_mu_);
+    auto it = wb_pending_.find(ref);
+    if (it != wb_pending_.end()) {
+      *out = it->second;
+      return Status::Ok();
+    }
+  }
+  return Store::GetBlob(ref, out);
+}
+
 Status FileStore::Get(const Ref& ref, std::vector<uint8_t>* out) {  // file.go:42-50
+  {
+    std::lock_guard<std::mutex> g(wb_mu_);
+    auto it = wb_pending_.find(ref);
+    if (it != wb_pending_.end()) {  // accepted by PutBlob, not written yet
+      out->assign(it->second.bytes(), it->second.bytes() + it->second.size);
+      return Status::Ok();
+    }
+  }
   const std::string path = BlobPath(ref);
   const int fd = ::open(path.c_str(), O_RDONLY);
   if (fd < 0) {
@@ -126,7 +219,7 @@ Status FileStore::Put(const uint8_t* data, size_t n, Ref* ref, bool* added) {  /
 Status FileStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) {
   if (added) *added = false;
   const std::string path = BlobPath(ref);
-  Status s = mkdir_all(path.substr(0, path.find_last_of('/')));
+  Status s = MkdirFor(path);
   if (!s.ok()) return s;
   const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0644);
   if (fd < 0) {
@@ -151,8 +244,10 @@ Status FileStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool
 
 // file.go:79-154: walk blobs/<2>/<4>/<64> in name order, starting after `start`.
 Status FileStore::ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) {
+  Status s = Flush();  // blobs accepted by PutBlob are listed once written
+  if (!s.ok()) return s;
   const std::string blobroot = root_ + "/blobs";
-  Status s = mkdir_all(blobroot);
+  s = mkdir_all(blobroot);
   if (!s.ok()) return s;
   std::vector<Entry> top, mid, blobs;
   s = read_dir(blobroot, &top);

@@ -637,6 +637,7 @@ Status Writer::Close() {  // split/split.go:104-126
   s = PutProto(root->node, &root_);
   if (!s.ok()) return sticky_ = s;
   levels_.clear();
+  if (rp_ && !(s = rp_->Flush()).ok()) return sticky_ = s;  // write-behind stores
   return Status::Ok();
 }
 
@@ -739,23 +740,44 @@ Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint
   w.cursor = std::move(cur);
   for (const Node& n : nodes) w.covered.push_back(n.offset);
   std::vector<std::vector<Blob>> chunks(nodes.size());
+  std::vector<std::pair<size_t, size_t>> all;  // (leaf node, leaf)
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    chunks[i].resize(nodes[i].leaves.size());
+    for (size_t k = 0; k < nodes[i].leaves.size(); ++k) all.emplace_back(i, k);
+  }
+  // fetched on up to 8 threads (store/file reads a file per chunk; store/mem only looks up)
+  std::vector<Status> errs(std::min<size_t>(8, std::max<size_t>(1, all.size() / 64)));
+  auto fetch = [&](size_t t) {
+    for (size_t x = t; x < all.size(); x += errs.size()) {
+      const size_t i = all[x].first, k = all[x].second;
+      Status s = g_->GetBlob(nodes[i].leaves[k].ref, &chunks[i][k]);
+      if (!s.ok()) {
+        errs[t] = Status::Err(s.code, "getting chunk: " + s.msg);
+        return;
+      }
+    }
+  };
+  if (errs.size() == 1) {
+    fetch(0);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < errs.size(); ++t) th.emplace_back(fetch, t);
+    for (std::thread& x : th) x.join();
+  }
+  for (const Status& e : errs)
+    if (!e.ok()) {
+      w.st = e;
+      return w;
+    }
   std::vector<const uint8_t*> ptrs;
   std::vector<uint64_t> lens;
   std::vector<const Ref*> want;
-  for (size_t i = 0; i < nodes.size(); ++i) {
-    const std::vector<Child>& leaves = nodes[i].leaves;
-    chunks[i].resize(leaves.size());
-    for (size_t k = 0; k < leaves.size(); ++k) {
-      Status s = g_->GetBlob(leaves[k].ref, &chunks[i][k]);
-      if (!s.ok()) {
-        w.st = Status::Err(s.code, "getting chunk: " + s.msg);
-        return w;
-      }
+  for (size_t i = 0; i < nodes.size(); ++i)
+    for (size_t k = 0; k < nodes[i].leaves.size(); ++k) {
       ptrs.push_back(chunks[i][k].bytes());
       lens.push_back(chunks[i][k].size);
-      want.push_back(&leaves[k].ref);
+      want.push_back(&nodes[i].leaves[k].ref);
     }
-  }
   std::vector<Ref> refs(ptrs.size());
   Status s = hasher_->SumPtrs(ptrs.data(), lens.data(), ptrs.size(), refs.data());
   if (!s.ok()) {

@@ -15,6 +15,7 @@
 #pragma once
 
 #include <array>
+#include <condition_variable>
 #include <deque>
 #include <cstddef>
 #include <cstdint>
@@ -24,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bsgpu.h"
@@ -81,6 +83,9 @@ class RefPutter {
   virtual Status PutBlob(const Ref& ref, const Blob& b, bool* added) {
     return PutWithRef(ref, b.bytes(), b.size, added);
   }
+  // Waits for blobs a store accepted without writing them yet (write-behind) and returns the
+  // first error among them. split.Writer.Close calls it.
+  virtual Status Flush() { return Status::Ok(); }
 };
 
 // Batched/one-off SHA-256 of host bytes on the GPU (bsg_hasher: persistent device buffers +
@@ -132,16 +137,36 @@ class FileStore : public Store, public RefPutter {
  public:
   explicit FileStore(std::string root, int device = 0)
       : root_(std::move(root)), hasher_(device) {}
+  ~FileStore() override;
   Status Get(const Ref& ref, std::vector<uint8_t>* out) override;
+  Status GetBlob(const Ref& ref, Blob* out) override;
   Status Put(const uint8_t* data, size_t n, Ref* ref, bool* added) override;
   Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
   Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
+  // Write-behind (split.Writer's chunks): the Blob is kept, and written by a pool of writer
+  // threads; Get sees it at once, Flush waits for the files. *added: not already pending.
+  Status PutBlob(const Ref& ref, const Blob& b, bool* added) override;
+  Status Flush() override;
   std::string BlobPath(const Ref& ref) const;
   const std::string& Root() const { return root_; }
 
  private:
+  Status MkdirFor(const std::string& path);  // os.MkdirAll of the blob's directory, cached
+  void Worker();
   std::string root_;
   GpuHasher hasher_;
+  std::mutex dir_mu_;
+  std::vector<bool> dirs_made_ = std::vector<bool>(1 << 16);  // blobs/hh/hhhh made, by hhhh
+  std::mutex wb_mu_;
+  std::condition_variable wb_cv_, wb_done_cv_;
+  std::deque<std::pair<Ref, Blob>> wb_queue_;
+  std::map<Ref, Blob> wb_pending_;  // accepted, not yet written
+  uint64_t wb_bytes_ = 0;           // bytes of wb_pending_ (bounded: kWriteBehindBytes)
+  Status wb_err_;
+  bool wb_stop_ = false;
+  std::vector<std::thread> wb_threads_;
+  static constexpr uint64_t kWriteBehindBytes = 1ull << 30;
+  static constexpr int kWriterThreads = 8;
 };
 
 bool RefFromHex(const std::string& hex, Ref* out);  // bs.RefFromHex (bs.go)
