@@ -1219,31 +1219,48 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
                          const uint32_t* table, bsg_chunk* out, uint64_t cap, uint64_t* counts,
                          uint64_t* nchunks) {
   if (nstreams && (!host_data || !off || !len)) return BSG_EINVAL;
+  if (!out && cap) return BSG_EINVAL;
   int rc;
   bsg_engine* e = bsg_engine_create(device, table, &rc);
   if (!e) return rc;
-  // pack streams 16-byte aligned into one device buffer
-  std::vector<uint64_t> doff(nstreams);
-  uint64_t total = 0;
-  for (uint32_t s = 0; s < nstreams; ++s) {
-    doff[s] = total;
-    total += (len[s] + 15) & ~15ull;
-  }
+  // Runs of at most 65,535 streams (the engine's limit) and about 8 GiB of device bytes (a
+  // larger stream goes alone); each run's streams are packed 16-byte aligned into one buffer.
+  constexpr uint32_t kRunStreams = 65535;
+  constexpr uint64_t kRunBytes = 8ull << 30;
   DevBuf d;
-  if (d.ensure(total + kReadSlack) != hipSuccess) {
-    bsg_engine_destroy(e);
-    return BSG_ENOMEM;
+  std::vector<uint64_t> doff;
+  uint64_t n = 0;  // records of all runs so far (written to out while they fit in cap)
+  for (uint32_t s0 = 0; s0 < nstreams && rc == BSG_OK;) {
+    uint32_t s1 = s0;
+    uint64_t total = 0;
+    doff.clear();
+    while (s1 < nstreams && s1 - s0 < kRunStreams &&
+           (s1 == s0 || total + len[s1] <= kRunBytes)) {
+      doff.push_back(total);
+      total += (len[s1] + 15) & ~15ull;
+      ++s1;
+    }
+    if (d.ensure(total + kReadSlack) != hipSuccess) {
+      rc = BSG_ENOMEM;
+      break;
+    }
+    for (uint32_t s = s0; s < s1 && rc == BSG_OK; ++s)
+      if (len[s] &&
+          hipMemcpy(static_cast<uint8_t*>(d.p) + doff[s - s0], host_data + off[s], len[s],
+                    hipMemcpyHostToDevice) != hipSuccess)
+        rc = BSG_EDEVICE;
+    uint64_t rn = 0;
+    if (rc == BSG_OK) rc = bsg_engine_run(e, d.as<uint8_t>(), doff.data(), len + s0, s1 - s0, params);
+    if (rc == BSG_OK) rc = bsg_engine_finish(e, &rn);
+    if (rc == BSG_OK && n < cap) {
+      rc = bsg_engine_copy_chunks(e, out + n, cap - n);
+      // records name their stream within the run: make them batch indices
+      for (uint64_t k = n; rc == BSG_OK && s0 && k < std::min(cap, n + rn); ++k) out[k].stream += s0;
+    }
+    if (rc == BSG_OK && counts) rc = bsg_engine_copy_counts(e, counts + s0, s1 - s0);
+    n += rn;
+    s0 = s1;
   }
-  for (uint32_t s = 0; s < nstreams && rc == BSG_OK; ++s)
-    if (len[s] &&
-        hipMemcpy(static_cast<uint8_t*>(d.p) + doff[s], host_data + off[s], len[s],
-                  hipMemcpyHostToDevice) != hipSuccess)
-      rc = BSG_EDEVICE;
-  uint64_t n = 0;
-  if (rc == BSG_OK) rc = bsg_engine_run(e, d.as<uint8_t>(), doff.data(), len, nstreams, params);
-  if (rc == BSG_OK) rc = bsg_engine_finish(e, &n);
-  if (rc == BSG_OK && out) rc = bsg_engine_copy_chunks(e, out, cap);
-  if (rc == BSG_OK && counts) rc = bsg_engine_copy_counts(e, counts, nstreams);
   if (nchunks) *nchunks = n;
   d.release();
   bsg_engine_destroy(e);

@@ -152,7 +152,10 @@ int bsg_engine_timeline(const bsg_engine* eng, uint64_t out[4]);
 /* Last run's candidate count (diagnostics). */
 uint64_t bsg_engine_candidates(const bsg_engine* eng);
 
-/* Convenience: split + hash host-resident streams (copies to the device), results to host. */
+/* Convenience: split + hash host-resident streams (copies to the device), results to host.
+ * Any number of streams: they run in groups of at most 65,535 streams and ~8 GiB. Records are
+ * in stream order, `stream` = the index in this call; at most cap are written, *nchunks is the
+ * total. */
 int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* off,
                          const uint64_t* len, uint32_t nstreams, const bsg_params* params,
                          const uint32_t* table, bsg_chunk* out, uint64_t cap, uint64_t* counts,

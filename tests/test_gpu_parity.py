@@ -132,6 +132,26 @@ def test_many_streams_past_lds_cache(gpu, oracle, table):
     assert k == len(ch)
 
 
+def test_batch_past_engine_stream_limit(gpu, oracle, table):
+    """140,000 host streams in one bsg_split_hash_batch call: more than an engine run takes
+    (65,535), so the batch runs in three groups; records keep their batch stream index and
+    every stream's chunks equal the oracle's."""
+    rng = np.random.default_rng(140_000)
+    lens = rng.integers(0, 2_500, size=140_000).astype(np.uint64)
+    lens[[0, 65_534, 65_535, 131_070, 139_999]] = [0, 5_000, 0, 1, 70_000]
+    base = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    arrs = [base[int(o):int(o) + int(n)] for o, n in zip(off, lens)]
+    ch, counts = gpu.split_hash_batch(arrs, bits=10, min_size=64)
+    want, wcounts = oracle.split_streams(table, base, off, [int(x) for x in lens], bits=10,
+                                         min_size=64, threads=8)
+    assert (counts == np.asarray(wcounts, dtype=np.uint64)).all()
+    assert len(ch) == len(want)
+    for f in ("offset", "len", "level", "ref"):
+        assert (ch[f] == want[f]).all(), f
+    assert (ch["stream"] == np.repeat(np.arange(len(lens)), counts.astype(np.int64))).all()
+
+
 def test_dense_candidates_zero_runs(gpu, oracle, table):
     """Long zero runs inside random data: every position in the run is a candidate."""
     from bs_amd.synth import splitmix_array
