@@ -1227,7 +1227,9 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
   // larger stream goes alone); each run's streams are packed 16-byte aligned into one buffer.
   constexpr uint32_t kRunStreams = 65535;
   constexpr uint64_t kRunBytes = 8ull << 30;
+  constexpr uint64_t kPackWindow = 64ull << 20;
   DevBuf d;
+  PinBuf pack;
   std::vector<uint64_t> doff;
   uint64_t n = 0;  // records of all runs so far (written to out while they fit in cap)
   for (uint32_t s0 = 0; s0 < nstreams && rc == BSG_OK;) {
@@ -1244,11 +1246,38 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
       rc = BSG_ENOMEM;
       break;
     }
-    for (uint32_t s = s0; s < s1 && rc == BSG_OK; ++s)
-      if (len[s] &&
-          hipMemcpy(static_cast<uint8_t*>(d.p) + doff[s - s0], host_data + off[s], len[s],
-                    hipMemcpyHostToDevice) != hipSuccess)
+    // Streams shorter than the pinned window are packed at their device offsets into it and
+    // copied a window at a time (one H2D for many small streams); longer ones directly.
+    const uint64_t win = std::min<uint64_t>(total, kPackWindow);
+    if (win && pack.ensure(win) != hipSuccess) {
+      rc = BSG_ENOMEM;
+      break;
+    }
+    uint64_t wlo = 0, whi = 0;  // device span [wlo, whi) staged in pack
+    auto flush = [&]() {
+      if (whi > wlo && hipMemcpy(static_cast<uint8_t*>(d.p) + wlo, pack.p, whi - wlo,
+                                 hipMemcpyHostToDevice) != hipSuccess)
         rc = BSG_EDEVICE;
+      wlo = whi;
+    };
+    for (uint32_t s = s0; s < s1 && rc == BSG_OK; ++s) {
+      const uint64_t at = doff[s - s0];
+      if (!len[s]) continue;
+      if (len[s] > win / 2) {
+        flush();
+        if (rc == BSG_OK &&
+            hipMemcpy(static_cast<uint8_t*>(d.p) + at, host_data + off[s], len[s],
+                      hipMemcpyHostToDevice) != hipSuccess)
+          rc = BSG_EDEVICE;
+        wlo = whi = at + len[s];
+        continue;
+      }
+      if (at + len[s] - wlo > win) flush();
+      if (whi == wlo) wlo = whi = at;
+      std::memcpy(pack.as<uint8_t>() + (at - wlo), host_data + off[s], len[s]);
+      whi = at + len[s];
+    }
+    if (rc == BSG_OK) flush();
     uint64_t rn = 0;
     if (rc == BSG_OK) rc = bsg_engine_run(e, d.as<uint8_t>(), doff.data(), len + s0, s1 - s0, params);
     if (rc == BSG_OK) rc = bsg_engine_finish(e, &rn);
@@ -1263,6 +1292,7 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
   }
   if (nchunks) *nchunks = n;
   d.release();
+  pack.release();
   bsg_engine_destroy(e);
   return rc;
 }
