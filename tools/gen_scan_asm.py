@@ -321,5 +321,147 @@ def write(L, path, name):
     print(path, len(L), "lines")
 
 
+
+
+# ---------------------------------------------------------------------------------------------
+# Round 2 EXPERIMENT, NOT IN THE BUILD: the block loop with whole lines requested TWO lines
+# ahead (tools/ubench/gen_scanload.py: 3.73 -> 3.06 ms per 16 GiB at two waves per SIMD; the
+# compiled form needs ~284 VGPRs). Wired into k_scan<true> as scan_lines2() it passed the GPU
+# parity tests (test_gpu_parity, test_gpu_configs, test_gpu_params: 90 tests), but a same-box A/B
+# gave configs[2]'s k_scan 3.68 / 3.82 ms against 3.71 / 3.69 for the compiled loop
+# (profiles/r02_scan_asm2_ab.log): in k_scan every 2 KiB strip restarts the pipeline (history,
+# first lines, the strip's stream descriptor), which the replay does not model. Fixed registers
+# v22..v255; the compiler keeps what lives across the statement in v0..v21.
+#   line j = blocks 2j, 2j+1 -> line buffer LB[j % 3] (lo half = block 2j); the 64 history bytes
+#   are block -1 (line -1, hi half). Block cb hashes with hin (out-going) / hcur (in-coming) and
+#   looks up block cb+1's bytes into hin; at the start of an even block cb = 2j, line j+2 is
+#   requested into the buffer line j-1 has left, so line j+1's words (first read at block 2j+1)
+#   were requested three blocks before they are used.
+# Per byte: rotl1 (alignbit), perm (LDS address byte*256 + lane*4), xor3 (bitop3), ds_read_b32;
+# per two bytes one v_min3_u16 of the low 16 bits (split_bits >= 16 pre-filter).
+L2_H, L2_H0, L2_M, L2_A, L2_HITS, L2_NM1 = (f"v{22 + i}" for i in range(6))
+L2_A0 = L2_A1 = L2_T = L2_A  # a DS / VMEM instruction reads its address VGPRs at issue
+L2_TPAIR, L2_TLO = "v[28:29]", "v28"
+L2_ADDR = "v[30:31]"
+L2_LB = (32, 64, 96)
+L2_HA, L2_HB = 128, 192
+L2_OUT = os.path.join(ROOT, "bs_amd", "csrc", "scan_lines2_loop.inc")
+
+
+def gen_lines2():
+    L = []
+    e = L.append
+
+    def wreg(x, k):  # VGPR holding byte k's word of block x
+        j = x // 2
+        return f"v{L2_LB[j % 3] + 16 * (x % 2) + (k >> 2)}"
+
+    def lds_read(dst, addr, k):
+        if k % 8 == 0:
+            e("s_waitcnt lgkmcnt(7)")  # at most 15 LDS reads in flight (lgkmcnt has 4 bits)
+        e(f"ds_read_b32 v{dst}, {addr}")
+
+    def set_addr(reg, block_sgpr):
+        e(f"v_min_u32 {L2_TLO}, {block_sgpr}, {L2_NM1}")
+        e(f"v_lshlrev_b32 {L2_TLO}, 6, {L2_TLO}")
+        e(f"v_lshl_add_u64 {reg}, {L2_TPAIR}, 0, %[base]")
+
+    def load_half(x, addr):
+        r0 = L2_LB[(x // 2) % 3] + 16 * (x % 2)
+        for q in range(4):
+            e(f"global_load_dwordx4 v[{r0 + 4 * q}:{r0 + 4 * q + 3}], {addr}, off offset:{16 * q}")
+
+    def load_line(first_block_sgpr_expr, x_even):
+        # blocks x, x+1 (clamped to the strip), both halves back to back: the line is fetched once
+        e(f"s_add_u32 %[sb], %[b], {first_block_sgpr_expr}")
+        set_addr(L2_ADDR, "%[sb]")
+        load_half(x_even, L2_ADDR)
+        e("s_add_u32 %[sb], %[sb], 1")
+        set_addr(L2_ADDR, "%[sb]")      # (the loads above read their address at issue)
+        load_half(x_even + 1, L2_ADDR)
+
+    def lookups(x, dst):
+        for k in range(64):
+            a = L2_A0 if k % 2 == 0 else L2_A1
+            e(f"v_perm_b32 {a}, {wreg(x, k)}, %[lane4], %[sel{k & 3}]")
+            lds_read(dst + k, a, k)
+
+    # ---- prologue: history (block -1), line 0, line 1 ----
+    e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    e("s_mov_b64 %[sexec], exec")
+    e(f"v_mov_b32 {L2_HITS}, 0")
+    e(f"v_add_u32 {L2_NM1}, -1, %[nfull]")
+    e("v_mov_b32 v29, 0")
+    e("s_mov_b32 %[b], 0")
+    hist = L2_LB[2] + 16
+    for q in range(4):
+        e(f"global_load_dwordx4 v[{hist + 4 * q}:{hist + 4 * q + 3}], %[pre], off offset:{16 * q}")
+    load_line(0, 0)
+    load_line(2, 2)
+    e("s_waitcnt vmcnt(16)")                   # the history landed
+    lookups(-1, L2_HA)                        # HA = table values of the history bytes
+    e("s_waitcnt vmcnt(8)")                    # line 0 landed
+    lookups(0, L2_HB)                         # HB = table values of block 0
+    e("s_waitcnt lgkmcnt(0)")
+    e(f"v_mov_b32 {L2_H}, 0")
+    for k in range(64):                       # h = hash of the history window
+        e(f"v_alignbit_b32 {L2_H}, {L2_H}, {L2_H}, 31")
+        e(f"v_xor_b32 {L2_H}, {L2_H}, v{L2_HA + k}")
+
+    def block(i):
+        # block cb = b + i (b a multiple of 6); its words are those of block i mod 6's slot
+        hin, hcur = (L2_HA, L2_HB) if i % 2 == 0 else (L2_HB, L2_HA)
+        if i == 0:
+            e(f"v_cmp_lt_u32 vcc, %[b], %[nfull]")
+        else:
+            e(f"s_add_u32 %[sb], %[b], {i}")
+            e("v_cmp_lt_u32 vcc, %[sb], %[nfull]")
+        e("s_and_b64 exec, exec, vcc")
+        e("s_cbranch_execz L_scan2_done_%=")
+        e("s_waitcnt vmcnt(8)")                # this block's lookups read block cb+1's words
+        if i % 2 == 0:                        # start of line j = cb/2: request line j+2
+            load_line(i + 4, i + 4)
+        e(f"v_mov_b32 {L2_M}, -1")
+        for k in range(0, 64, 2):
+            for j, (dst, src) in enumerate(((L2_H0, L2_H), (L2_H, L2_H0))):
+                kk = k + j
+                a = L2_A0 if j == 0 else L2_A1
+                e(f"v_alignbit_b32 {dst}, {src}, {src}, 31")
+                e(f"v_perm_b32 {a}, {wreg(i + 1, kk)}, %[lane4], %[sel{kk & 3}]")
+                e(f"v_bitop3_b32 {dst}, {dst}, v{hin + kk}, v{hcur + kk} bitop3:0x96")
+                lds_read(hin + kk, a, kk)
+            e(f"v_min3_u16 {L2_M}, {L2_M}, {L2_H0}, {L2_H}")
+        e(f"v_cmp_eq_u16 vcc, 0, {L2_M}")
+        e(f"s_lshl_b32 %[sb], {1 << i}, %[b]")
+        e(f"v_mov_b32 {L2_T}, %[sb]")
+        e(f"v_cndmask_b32 {L2_T}, 0, {L2_T}, vcc")
+        e(f"v_or_b32 {L2_HITS}, {L2_HITS}, {L2_T}")
+
+    e("L_scan2_loop_%=:")
+    for i in range(6):
+        block(i)
+    e("s_add_u32 %[b], %[b], 6")
+    e("s_branch L_scan2_loop_%=")
+    e("L_scan2_done_%=:")
+    e("s_mov_b64 exec, %[sexec]")
+    e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    e(f"v_mov_b32 %[hits], {L2_HITS}")
+    nvalu = sum(1 for l in L if l.startswith("v_"))
+    with open(L2_OUT, "w") as f:
+        f.write("// GENERATED by tools/gen_scan_asm.py (gen_lines2) -- do not edit.\n")
+        f.write(f"// k_scan full-block loop, lines requested two ahead: {len(L)} lines, {nvalu} VALU.\n")
+        f.write("#define BSG_SCAN_LINES2_ASM \\\n")
+        for l in L:
+            f.write(f'  "{l}\\n" \\\n')
+        f.write('  ""\n')
+        f.write("#define BSG_SCAN_LINES2_CLOBBERS " +
+                ", ".join(f'"v{r}"' for r in range(22, 256)) + ', "vcc", "scc"\n')
+    print(L2_OUT, len(L), "lines", nvalu, "VALU")
+
+
 if __name__ == "__main__":
-    main()
+    import sys
+    if len(sys.argv) > 1 and sys.argv[1] == "lines2":
+        gen_lines2()
+    else:
+        main()
