@@ -343,19 +343,39 @@ __device__ __forceinline__ StripLoc locate(const ScanArgs& a, uint64_t strip, ld
   return l;
 }
 
+// Where a strip's bytes are and what its segment needs, for the fast pass: located and read from
+// the stream descriptor one strip AHEAD of its scan (k_scan's loop), so the binary search and the
+// descriptor loads run behind the current strip's scan instead of stalling both waves of every
+// SIMD at each strip start.
+struct StripJob {
+  const uint8_t* d;    // the segment's first byte
+  const uint8_t* pre;  // the 64 bytes before the strip (the segment history for its first strip)
+  uint64_t start;      // segment offset of the strip
+  uint32_t len;        // bytes in the strip
+  bool tail;           // k_refine has the segment's < 64-byte tail or the final flush here
+};
+
+__device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip, lds_u64p s0) {
+  const StripLoc l = locate(a, strip, s0);
+  const StreamDesc* sd = a.streams + l.stream;
+  StripJob j;
+  j.d = a.data + sd->data_off;
+  j.pre = l.start >= 64 ? j.d + l.start - 64 : sd->hist;
+  j.start = l.start;
+  j.len = l.len;
+  j.tail = (l.len & 63u) != 0 || (l.last && sd->finalize);
+  return j;
+}
+
 // Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
 // hit bit per block whose pre-filter fires. Writes counts[strip] = 0 and returns whether
 // k_refine has exact work for the strip (hit blocks, the segment's < 64-byte tail, or the
 // final chunk's flush), with the hit mask in *hits_out.
 template <bool WIDE>
 __device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                                           uint64_t strip, lds_u64p s0, uint32_t* hits_out) {
-  const StripLoc l = locate(a, strip, s0);
-  const StreamDesc* sd = a.streams + l.stream;
-  const uint8_t* d = a.data + sd->data_off;
+                                           uint64_t strip, const StripJob& j, uint32_t* hits_out) {
   uint32_t w[16];
-  if (l.start >= 64) load16(d + l.start - 64, w);
-  else load16(sd->hist, w);
+  load16(j.pre, w);
   uint32_t hist[64];
   uint32_t h = 0;
 #pragma unroll
@@ -364,13 +384,12 @@ __device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* ta
     h = rotl1(h) ^ t;
     hist[k] = t;
   }
-  const uint32_t nfull = l.len >> 6;
+  const uint32_t nfull = j.len >> 6;
   uint32_t hits = 0;
-  if (nfull) hits = scan_full_blocks<WIDE>(a, tab, lane4, d + l.start, nfull, h, hist);
-  const bool tail = (l.len & 63u) != 0 || (l.last && sd->finalize);
+  if (nfull) hits = scan_full_blocks<WIDE>(a, tab, lane4, j.d + j.start, nfull, h, hist);
   a.counts[strip] = 0u;
   *hits_out = hits;
-  return hits || tail;
+  return hits || j.tail;
 }
 
 // Appends the flagged strips of a wave to the refine list, one atomic per wave: entry =
@@ -445,11 +464,17 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
-  for (uint64_t g = blockIdx.x; g * kScanWG < a.nstrips; g += gridDim.x) {
+  uint64_t g = blockIdx.x;
+  StripJob job{};
+  if (g * kScanWG + threadIdx.x < a.nstrips) job = strip_job(a, g * kScanWG + threadIdx.x, s0);
+  for (; g * kScanWG < a.nstrips; g += gridDim.x) {
     const uint64_t strip = g * kScanWG + threadIdx.x;
+    const StripJob cur = job;
+    const uint64_t next = strip + (uint64_t)gridDim.x * kScanWG;
+    if (next < a.nstrips) job = strip_job(a, next, s0);  // used one iteration later
     bool flag = false;
     uint32_t hits = 0;
-    if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, s0, &hits);
+    if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, cur, &hits);
     refine_append(a, flag, strip, hits);
   }
 }

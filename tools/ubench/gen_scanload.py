@@ -48,7 +48,24 @@ def loads(buf: int) -> list[str]:
     return L
 
 
-def kernel(name: str, load: bool, lds: bool, ahead: int = 1) -> list[str]:
+def restart(hist: int) -> list[str]:
+    """k_scan's per-strip start: drain, load the 64 history bytes, look them up, fold the hash."""
+    L = ["s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    L += [f"global_load_dwordx4 v[{hist + 4 * q}:{hist + 4 * q + 3}], v[{AD}:{AD + 1}], off offset:{16 * q}"
+          for q in range(4)]
+    L += ["s_waitcnt vmcnt(0)"]
+    for k in range(64):
+        L.append(f"v_perm_b32 v40, v{hist + (k >> 2)}, v12, s{8 + (k & 3)}")
+        L.append(f"ds_read_b32 v{16 + (k % RING)}, v40")
+        L.append("s_waitcnt lgkmcnt(14)")
+    L += ["s_waitcnt lgkmcnt(0)"]
+    for k in range(64):
+        L.append("v_alignbit_b32 v1, v1, v1, 31")
+        L.append(f"v_xor_b32 v1, v1, v{16 + (k % RING)}")
+    return L
+
+
+def kernel(name: str, load: bool, lds: bool, ahead: int = 1, every: int = 0) -> list[str]:
     global AD
     AD = 108 if ahead == 1 else 140  # (<= 128 VGPRs with two buffers: 4 waves per SIMD fit)
     A, B, C = 44, 76, 108
@@ -66,19 +83,26 @@ def kernel(name: str, load: bool, lds: bool, ahead: int = 1) -> list[str]:
         pro += loads(A) + loads(B)
         for cur, nxt in ((A, C), (B, A), (C, B)):
             body += loads(nxt) + ["s_waitcnt vmcnt(16)"] + line_body(cur, lds)
-    asm = "\\n".join(pro + [".Lloop%=:"] + body +
+    if every:  # a strip restart every `every` iterations (s18 counts them)
+        hist = AD + 2
+        body = (["s_add_u32 s18, s18, 1", f"s_cmp_eq_u32 s18, {every}", "s_cbranch_scc0 .Lnors%=",
+                 "s_mov_b32 s18, 0"] + restart(hist) + [".Lnors%=:"] + body)
+    asm = "\\n".join(pro + ["s_mov_b32 s18, 0", ".Lloop%=:"] + body +
                      ["s_sub_u32 s13, s13, 1", "s_cmp_lg_u32 s13, 0", "s_cbranch_scc1 .Lloop%="])
     regs = ["v1", "v2", "v3", "v12", "v40", f"v{AD}", f"v{AD + 1}"] + \
-        [f"v{r}" for r in range(16, 40)] + [f"v{r}" for r in range(44, AD)]
+        [f"v{r}" for r in range(16, 40)] + [f"v{r}" for r in range(44, AD)] + \
+        ([f"v{r}" for r in range(AD + 2, AD + 18)] if every else [])
     clob = ", ".join(f'"{r}"' for r in regs)
     return [
-        f'__global__ __launch_bounds__(1024) void k_{name}(const uint8_t* buf, uint32_t* sink, int iters, uint32_t jump) {{',
+        f'__global__ __launch_bounds__(1024) void k_{name}(const uint8_t* buf, uint32_t* sink, int iters, uint32_t jump, uint64_t* clk) {{',
         '  extern __shared__ uint32_t tab[];',
         '  for (int i = threadIdx.x; i < 16384; i += blockDim.x) tab[i] = i * 2654435761u;',
         '  __syncthreads();',
         '  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;',
         '  const uint8_t* p = buf + gid * 2048;',
         '  uint32_t o;',
+        '  uint64_t t0, r0, t1, r1;',
+        '  asm volatile("s_memtime %0\\n s_memrealtime %1\\n s_waitcnt lgkmcnt(0)" : "=s"(t0), "=s"(r0) :: "memory");',
         '  asm volatile(',
         '    "v_mov_b32 v1, %1\\n v_mov_b32 v2, %1\\n v_mov_b32 v3, -1\\n"',
         '    "v_lshlrev_b32 v12, 2, %1\\n v_and_b32 v12, 0xfc, v12\\n"',
@@ -88,17 +112,20 @@ def kernel(name: str, load: bool, lds: bool, ahead: int = 1) -> list[str]:
         f'    "{asm}\\n"',
         '    "s_waitcnt vmcnt(0) lgkmcnt(0)\\n v_xor_b32 %0, v3, v44\\n"',
         '    : "=v"(o) : "v"(threadIdx.x), "s"(iters), "s"(jump), "v"((uint32_t)(uintptr_t)p), "v"((uint32_t)((uintptr_t)p >> 32))',
-        f'    : "memory", "vcc", "s8", "s9", "s10", "s11", "s13", "s14", "s15", "s16", "s17", {clob});',
+        f'    : "memory", "vcc", "s8", "s9", "s10", "s11", "s13", "s14", "s15", "s16", "s17", "s18", {clob});',
+        '  asm volatile("s_memtime %0\\n s_memrealtime %1\\n s_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1) :: "memory");',
         '  sink[gid & 1023] = o;',
+        '  if (gid == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }',
         '}', '']
 
 
 src = ['// Generated by gen_scanload.py: k_scan per-byte pattern with its HBM stream, whole chip.',
        '#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <cstdint>', '']
-VARIANTS = (("full", True, True, 1), ("noload", False, True, 1), ("nolds", True, False, 1),
-            ("full2a", True, True, 2), ("nolds2a", True, False, 2))
-for name, load, lds, ahead in VARIANTS:
-    src += kernel(name, load, lds, ahead)
+VARIANTS = (("full", True, True, 1, 0), ("noload", False, True, 1, 0), ("nolds", True, False, 1, 0),
+            ("full2a", True, True, 2, 0), ("nolds2a", True, False, 2, 0),
+            ("full_rs", True, True, 1, 8), ("full2a_rs", True, True, 2, 5))
+for name, load, lds, ahead, every in VARIANTS:
+    src += kernel(name, load, lds, ahead, every)
 src += [
     'template <typename K> void run(K k, const char* name, int wps, const uint8_t* buf, uint32_t* s, int lpi = 2) {',
     '  const int grid = 256, threads = 64 * 4 * wps;',
@@ -107,24 +134,34 @@ src += [
     '  int iters = (int)((4ull << 30) / (lanes * 128 * lpi)) & ~7;',
     '  const uint32_t jump = (uint32_t)(lanes * 2048 - 15 * 128);',
     '  hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);',
-    '  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 98304, 0, buf, s, iters, jump);',
+    '  uint64_t* clk; hipMalloc(&clk, 16);',
+    '  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 98304, 0, buf, s, iters, jump, clk);',
     '  hipEventRecord(a);',
-    '  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 98304, 0, buf, s, iters, jump);',
+    '  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 98304, 0, buf, s, iters, jump, clk);',
     '  hipEventRecord(b); hipEventSynchronize(b);',
     '  float ms = 0; hipEventElapsedTime(&ms, a, b); ms /= 3;',
     '  const double bytes = (double)lanes * iters * 128 * lpi;',
-    '  printf("%-7s waves/SIMD=%d  %.2f TB/s  -> 16 GiB in %.2f ms  (%.1f MiB per launch, %.3f ms)\\n", name, wps,',
-    '         bytes / (ms * 1e-3) / 1e12, (16.0 * (1ull << 30)) / (bytes / (ms * 1e-3)) * 1e3, bytes / 1048576.0, ms);',
+    '  uint64_t c[2]; hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost); hipFree(clk);',
+    '  printf("%-9s waves/SIMD=%d  %.2f TB/s  -> 16 GiB in %.2f ms  (%.1f MiB per launch, %.3f ms, clock %.2f GHz)\\n", name, wps,',
+    '         bytes / (ms * 1e-3) / 1e12, (16.0 * (1ull << 30)) / (bytes / (ms * 1e-3)) * 1e3, bytes / 1048576.0, ms,',
+    '         c[1] ? (double)c[0] / ((double)c[1] * 10.0) : 0.0);',
     '}',
     'int main() {',
     '  uint8_t* buf; uint32_t* s;',
     '  const size_t n = (5ull << 30) + (64u << 20);',
     '  hipMalloc(&buf, n); hipMalloc(&s, 4096); hipMemset(buf, 0x5a, n);',
-    '  for (int w : {2, 3, 4}) run(k_full, "full", w, buf, s);',
-    '  for (int w : {2, 3, 4}) run(k_noload, "noload", w, buf, s);',
-    '  for (int w : {2, 3, 4}) run(k_nolds, "nolds", w, buf, s);',
-    '  for (int w : {2, 3}) run(k_full2a, "full2a", w, buf, s, 3);',
-    '  for (int w : {2, 3}) run(k_nolds2a, "nolds2a", w, buf, s, 3);',
+    '  // pass 0 warms the clocks and the buffer up (the first launches over a fresh 5 GiB buffer',
+    '  // ran ~20 % slower than the same kernel later in the run); pass 1 is the one to read',
+    '  for (int pass = 0; pass < 2; ++pass) {',
+    '    printf("pass %d\\n", pass);',
+    '    for (int w : {2, 3, 4}) run(k_full, "full", w, buf, s);',
+    '    for (int w : {2, 3, 4}) run(k_noload, "noload", w, buf, s);',
+    '    for (int w : {2, 3, 4}) run(k_nolds, "nolds", w, buf, s);',
+    '    for (int w : {2, 3}) run(k_full2a, "full2a", w, buf, s, 3);',
+    '    for (int w : {2, 3}) run(k_nolds2a, "nolds2a", w, buf, s, 3);',
+    '    for (int w : {2}) run(k_full_rs, "full_rs", w, buf, s);',
+    '    for (int w : {2}) run(k_full2a_rs, "full2a_rs", w, buf, s, 3);',
+    '  }',
     '  hipFree(buf); hipFree(s);',
     '  return 0;',
     '}']
