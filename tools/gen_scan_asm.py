@@ -325,12 +325,12 @@ def write(L, path, name):
 
 # ---------------------------------------------------------------------------------------------
 # Round 2 EXPERIMENT, NOT IN THE BUILD: the block loop with whole lines requested TWO lines
-# ahead (tools/ubench/gen_scanload.py: 3.73 -> 3.06 ms per 16 GiB at two waves per SIMD; the
-# compiled form needs ~284 VGPRs). Wired into k_scan<true> as scan_lines2() it passed the GPU
+# ahead (a first replay run, tools/ubench/gen_scanload.py, showed 3.73 -> 3.06 ms per 16 GiB;
+# that was the GPU clock ramping up during the first launches, at full clock both take ~3.0 ms;
+# the compiled form needs ~284 VGPRs). Wired into k_scan<true> as scan_lines2() it passed the GPU
 # parity tests (test_gpu_parity, test_gpu_configs, test_gpu_params: 90 tests), but a same-box A/B
 # gave configs[2]'s k_scan 3.68 / 3.82 ms against 3.71 / 3.69 for the compiled loop
-# (profiles/r02_scan_asm2_ab.log): in k_scan every 2 KiB strip restarts the pipeline (history,
-# first lines, the strip's stream descriptor), which the replay does not model. Fixed registers
+# (profiles/r02_scan_asm2_ab.log), as the clock-corrected replay predicts. Fixed registers
 # v22..v255; the compiler keeps what lives across the statement in v0..v21.
 #   line j = blocks 2j, 2j+1 -> line buffer LB[j % 3] (lo half = block 2j); the 64 history bytes
 #   are block -1 (line -1, hi half). Block cb hashes with hin (out-going) / hcur (in-coming) and

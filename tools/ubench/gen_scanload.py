@@ -7,8 +7,11 @@ Per lane: 2 KiB strips, whole 128-byte lines loaded one line ahead (8 x global_l
 into two 32-register line buffers, as k_scan), after 16 lines the next strip of the grid.
 Per byte: v_perm (LDS address byte*256 + lane*4), ds_read_b32 into a 16-deep lookup ring
 (lgkmcnt(14)), v_alignbit (rotl 1), v_bitop3 (xor3); per two bytes one v_min3_u16.
-Variants: full; no loads (words stay in registers); no LDS (a v_mov instead of the lookup).
-Output: TB/s and the time the loop would take for 16 GiB (configs[2]; k_scan: 3.7 ms).
+Variants: full; no loads (words stay in registers); no LDS (a v_mov instead of the lookup); lines
+requested two ahead (three line buffers); a strip restart every 2 KiB (drain, history load,
+lookups, hash warm-up). Every variant runs twice: the first pass warms the clock up (its first
+launches ran at 1.5-1.7 GHz), the second pass is the one to read.
+Output: TB/s, the time for 16 GiB (configs[2]; k_scan: 3.7 ms) and the launch's clock.
 """
 import os
 
