@@ -10,6 +10,11 @@ that stream: rolling-hash scan -> MinSize boundary selection -> SHA-256 of every
 data path (weak scaling); torch.distributed is used only for the barrier and the max-over-ranks
 timing.
 
+The default N=1 run then times configs[2] (256 x 64 MiB streams on the same GPU: the many-blob
+path, the largest single-GPU config) the same way, after freeing the configs[1] buffers, and
+reports it as the nested "configs2" record of the same JSON line (its own value, ms_per_step,
+stage times, roofline and 16-thread CPU baseline). The headline value stays configs[1].
+
   python bench.py [--gpus N] [--steps K] [--warmup W]
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 """
@@ -44,9 +49,15 @@ def parse():
     ap.add_argument("--e2e-mib", type=int, default=1024,
                     help="bytes of host-memory stream for the PCIe-inclusive streaming rate "
                          "(bsg_write -> records in host memory; 0: skip)")
+    ap.add_argument("--configs2-steps", type=int, default=None,
+                    help="timed steps of the nested configs[2] record (256 x 64 MiB on the same "
+                         "GPU, N=1 default run only; default: --steps, 0: skip)")
     ap.add_argument("--check", action="store_true",
                     help="verify the device records against the CPU oracle after timing")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.configs2_steps is None:
+        a.configs2_steps = a.steps
+    return a
 
 
 def dist_setup():
@@ -254,7 +265,7 @@ def pmc_traffic(kernel: str, workload: str):
                 doc = json.load(f)
         except (OSError, ValueError):
             continue
-        if not workload.startswith(doc.get("workload", "\0")):
+        if doc.get("workload", "\0") not in workload:
             continue
         ks = [doc.get("kernels", {}).get(n) for n in names]
         ks = [k for k in ks if k]
@@ -263,16 +274,25 @@ def pmc_traffic(kernel: str, workload: str):
     return None, None
 
 
-def main():
-    args = parse()
-    world, rank, local = dist_setup()
-    check_world(args.gpus, world)
-    from bs_amd import bsgpu
+CONFIGS1 = "configs[1]: 1 GiB random stream per GPU, default split params"
+CONFIGS2 = "configs[2]: 256 x 64 MiB streams per GPU"
+STAGES = ["k_scan", "k_compact+k_select+k_chunks+prefix", "k_sha"]
 
-    build_once(world, local)
-    assert bsgpu.device_count() > local, "bench.py needs a GPU (the HIP path is the product)"
-    nbytes = args.stream_mib << 20
-    ns = args.streams
+
+def workload_name(ns: int, nbytes: int, bits: int, min_size: int) -> str:
+    if bits == 16 and min_size == 1024 and ns == 1 and nbytes == 1 << 30:
+        return CONFIGS1
+    if bits == 16 and min_size == 1024 and ns == 256 and nbytes == 64 << 20:
+        return CONFIGS2
+    return f"{ns} x {nbytes >> 20} MiB streams per GPU"
+
+
+def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmup: int,
+               world: int, rank: int, local: int, cpu_sample: int, check: bool) -> dict:
+    """One device-resident workload: ns streams of nbytes generated in HBM, W warmups, K timed
+    steps (each a full scan -> select -> SHA-256 pass, records left in HBM), then the CPU
+    baseline over a bounded sample of the same bytes. Frees its device memory before returning."""
+    from bs_amd import bsgpu
     stride = (nbytes + 15) & ~15
     buf = bsgpu.DeviceBuffer(stride * ns, device=local)
     eng = bsgpu.Engine(device=local)
@@ -286,7 +306,7 @@ def main():
     nsteps = [0]
 
     def step():
-        eng.run(buf.ptr, offs, lens, bits=args.bits, min_size=args.min_size)
+        eng.run(buf.ptr, offs, lens, bits=bits, min_size=min_size)
         eng.finish()  # waits on the engine's stream; records stay in HBM
         ms = eng.stage_ms()
         for i in range(3):
@@ -297,53 +317,96 @@ def main():
         bsgpu.synchronize(local)
 
     # warmup steps are counted into stage_sum too; reset after them
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     stage_sum[:] = [0.0, 0.0, 0.0]
     nsteps[0] = 0
-    elapsed = timed_steps(step, sync, world, args.steps, 0)
-    total_bytes = world * ns * nbytes * args.steps
-    value = total_bytes / elapsed / 2**30
+    elapsed = timed_steps(step, sync, world, steps, 0)
     stage_avg = [s / max(nsteps[0], 1) for s in stage_sum]
-    names = ["k_scan", "k_compact+k_select+k_chunks+prefix", "k_sha"]
-    dom = max(range(3), key=lambda i: stage_avg[i])
-    per_launch_bytes = ns * nbytes  # algorithmic: every input byte read once by the kernel
-    achieved = per_launch_bytes / (stage_avg[dom] * 1e-3) / 1e9 if stage_avg[dom] > 0 else 0.0
-    chunks = eng.nchunks
-    check = None
-    if args.check and rank == 0:
+    ok = None
+    if check and rank == 0:
         from bs_amd.synth import splitmix_array
-        from oracle import oracle as O
-        ref = O.split(O.buzhash32_table(1), splitmix_array(BASE_SEED, nbytes), bits=args.bits,
-                      min_size=args.min_size)
+        from oracle import oracle as O  # checker only, after timing
+        ref = O.split(O.buzhash32_table(1), splitmix_array(BASE_SEED, nbytes), bits=bits,
+                      min_size=min_size)
         got = eng.chunks()[: len(ref)] if ns == 1 else eng.chunks()[: eng.counts()[0]]
-        check = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
-                     and (got["offset"] == ref["offset"]).all())
+        ok = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
+                  and (got["offset"] == ref["offset"]).all())
     diag = eng.diag()
+    chunks = int(eng.nchunks)
     # the CPU baseline's sample: the same device bytes, copied back after timing
     host_streams, sample = [], ""
-    if rank == 0 and world == 1 and args.cpu_sample_mib > 0:
-        want = args.cpu_sample_mib << 20
+    if rank == 0 and world == 1 and cpu_sample > 0:
+        want = cpu_sample << 20
         if ns == 1:
             host_streams = [buf.to_host(0, min(nbytes, want))]
             sample = f"first {len(host_streams[0]) >> 20} MiB of stream 0"
         else:
             k = min(ns, max(4 * cpu_threads(), -(-want // nbytes)))
             host_streams = [buf.to_host(offs[i], nbytes) for i in range(k)]
-            sample = f"streams 0..{k - 1} of {ns} ({k} x {args.stream_mib} MiB)"
-    # the device-resident engine and its input are done with: free them, so the streaming
-    # measurement below has the GPU's hardware queues and memory to itself
+            sample = f"streams 0..{k - 1} of {ns} ({k} x {nbytes >> 20} MiB)"
+    # the engine and its input are done with: free them before the next leg
     eng.close()
     buf.free()
-    cpu = cpu_baseline(host_streams, args.bits, args.min_size, sample)
+    cpu = cpu_baseline(host_streams, bits, min_size, sample)
     del host_streams
+    return {"elapsed": elapsed, "stage_avg": stage_avg, "diag": diag, "chunks": chunks,
+            "check": ok, "cpu": cpu}
+
+
+def roofline(workload: str, per_launch_bytes: int, stage_avg: list) -> dict:
+    """The dominant kernel's algorithmic bytes per launch / its event-timed duration, against
+    the 8 TB/s HBM peak; k_scan beside it. traffic = HBM bytes per launch from the newest
+    committed PMC summary of the same workload (profiles/rNN*_pmc.json)."""
+    dom = max(range(3), key=lambda i: stage_avg[i])
+    achieved = per_launch_bytes / (stage_avg[dom] * 1e-3) / 1e9 if stage_avg[dom] > 0 else 0.0
+    scan_gbs = per_launch_bytes / (stage_avg[0] * 1e-3) / 1e9 if stage_avg[0] > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(STAGES[dom], workload)
+    scan_traffic, _ = pmc_traffic("k_scan", workload)
+    return {"bound": "hbm", "kernel": STAGES[dom],
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_unit": "bytes/launch", "traffic_src": traffic_src,
+            "algorithmic_bytes": per_launch_bytes,
+            "limiter": "longest chunk's serial SHA-256 chain (issue latency)",
+            "k_scan": {"achieved": round(scan_gbs, 1), "frac": round(scan_gbs / HBM_PEAK_GBS, 4),
+                       "traffic": scan_traffic}}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup()
+    check_world(args.gpus, world)
+    from bs_amd import bsgpu
+
+    build_once(world, local)
+    assert bsgpu.device_count() > local, "bench.py needs a GPU (the HIP path is the product)"
+    nbytes = args.stream_mib << 20
+    ns = args.streams
+    leg = device_leg(ns, nbytes, args.bits, args.min_size, args.steps, args.warmup, world, rank,
+                     local, args.cpu_sample_mib, args.check)
+    elapsed, stage_avg = leg["elapsed"], leg["stage_avg"]
+    total_bytes = world * ns * nbytes * args.steps
+    value = total_bytes / elapsed / 2**30
+    workload = workload_name(ns, nbytes, args.bits, args.min_size)
+    # configs[2] (the largest single-GPU config, the many-blob path) on the same GPU, timed the
+    # same way, as a nested record; the headline stays configs[1]
+    c2 = None
+    if (rank == 0 and world == 1 and workload == CONFIGS1 and args.configs2_steps > 0):
+        n2, ns2 = 64 << 20, 256
+        leg2 = device_leg(ns2, n2, 16, 1024, args.configs2_steps, args.warmup, 1, 0, local,
+                          args.cpu_sample_mib, False)
+        c2 = {"workload": CONFIGS2,
+              "value": round(ns2 * n2 * args.configs2_steps / leg2["elapsed"] / 2**30, 3),
+              "unit": "GiB/s", "steps": args.configs2_steps, "warmup": args.warmup,
+              "ms_per_step": round(leg2["elapsed"] * 1e3 / args.configs2_steps, 3),
+              "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, leg2["stage_avg"])},
+              "chunks_per_step": leg2["chunks"],
+              "roofline": roofline(CONFIGS2, ns2 * n2, leg2["stage_avg"]),
+              "cpu_baseline": leg2["cpu"], "sha_path": leg2["diag"],
+              "chain_roofline": chain_roofline(leg2["diag"])}
     e2e = end_to_end(args.e2e_mib, args.bits, args.min_size, local) \
         if (rank == 0 and world == 1) else None
-    workload = ("configs[1]: 1 GiB random stream per GPU, default split params"
-                if (ns == 1 and nbytes == 1 << 30 and args.bits == 16 and args.min_size == 1024)
-                else f"{ns} x {args.stream_mib} MiB streams per GPU")
-    traffic, traffic_src = pmc_traffic(names[dom], workload)
-    scan_gbs = per_launch_bytes / (stage_avg[0] * 1e-3) / 1e9 if stage_avg[0] > 0 else 0.0
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -362,23 +425,17 @@ def main():
                        "stream_bytes": nbytes, "streams_per_gpu": ns,
                        "split_bits": args.bits, "min_size": args.min_size, "fanout": 8,
                        "parallelism": "independent streams, one set per GPU, no collectives"},
-            "roofline": {"bound": "hbm", "kernel": names[dom],
-                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_unit": "bytes/launch", "traffic_src": traffic_src,
-                         "algorithmic_bytes": per_launch_bytes,
-                         "limiter": "longest chunk's serial SHA-256 chain (issue latency)",
-                         "k_scan": {"achieved": round(scan_gbs, 1),
-                                    "frac": round(scan_gbs / HBM_PEAK_GBS, 4)}},
-            "cpu_baseline": cpu,
+            "roofline": roofline(workload, ns * nbytes, stage_avg),
+            "cpu_baseline": leg["cpu"],
             "end_to_end": e2e,
-            "stage_ms": {n: round(v, 4) for n, v in zip(names, stage_avg)},
-            "chunks_per_step": int(chunks),
-            "sha_path": diag,
-            "chain_roofline": chain_roofline(diag),
+            "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, stage_avg)},
+            "chunks_per_step": leg["chunks"],
+            "sha_path": leg["diag"],
+            "chain_roofline": chain_roofline(leg["diag"]),
+            "configs2": c2,
         }
-        if check is not None:
-            line["oracle_check"] = check
+        if leg["check"] is not None:
+            line["oracle_check"] = leg["check"]
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -113,6 +113,8 @@ def lib() -> ctypes.CDLL:
         "bsg_filestore_new": (vp, [ctypes.c_char_p, ctypes.c_int]),
         "bsg_store_free": (None, [vp]),
         "bsg_store_count": (ctypes.c_size_t, [vp]),
+        "bsg_filestore_set_write_behind": (ctypes.c_int, [vp, ctypes.c_uint64]),
+        "bsg_store_held_bytes": (ctypes.c_size_t, [vp]),
         "bsg_store_get": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t,
                                          ctypes.POINTER(ctypes.c_size_t)]),
         "bsg_store_put": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp,
@@ -540,6 +542,10 @@ class MemStore:
     def __len__(self) -> int:
         return lib().bsg_store_count(self.h)
 
+    def held_bytes(self) -> int:
+        """Host bytes the store keeps alive (store/mem: copies + aliased Write pieces)."""
+        return lib().bsg_store_held_bytes(self.h)
+
     def delete(self, ref: bytes) -> None:
         """bs.DeleterStore.Delete (store/mem only)."""
         _check(lib().bsg_store_delete(self.h, bytes(ref)), "Delete")
@@ -577,6 +583,9 @@ class FileStore(MemStore):
         self.h = lib().bsg_filestore_new(os.fsencode(root), device)
         if not self.h:
             raise BsgError(-22, "bsg_filestore_new")
+
+    def set_write_behind(self, nbytes: int) -> None:
+        _check(lib().bsg_filestore_set_write_behind(self.h, nbytes), "set_write_behind")
 
 
 class Writer:

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
 #include <cstring>
 
 #include "../../include/bs_split.hpp"
@@ -90,10 +91,15 @@ std::string FileStore::BlobPath(const Ref& ref) const {  // file.go:33-40
 }
 
 FileStore::~FileStore() {
-  (void)Flush();
+  (void)FlushAll();
   {
     std::lock_guard<std::mutex> g(wb_mu_);
     wb_stop_ = true;
+    // errors no caller has collected with Flush: nobody is left to return them to
+    for (const auto& kv : groups_)
+      if (!kv.second.err.ok())
+        std::fprintf(stderr, "bs::FileStore(%s): unreported write error (group %llu): %s\n",
+                     root_.c_str(), (unsigned long long)kv.first, kv.second.err.msg.c_str());
   }
   wb_cv_.notify_all();
   for (std::thread& t : wb_threads_) t.join();
@@ -115,19 +121,60 @@ Status FileStore::MkdirFor(const std::string& path) {
   return Status::Ok();
 }
 
-Status FileStore::PutBlob(const Ref& ref, const Blob& b, bool* added) {
-  std::unique_lock<std::mutex> g(wb_mu_);
-  if (!wb_err_.ok()) return wb_err_;
+uint64_t FileStore::OpenGroup() {
+  std::lock_guard<std::mutex> g(wb_mu_);
+  const uint64_t id = next_group_++;
+  groups_[id] = Group{};
+  return id;
+}
+
+void FileStore::CloseGroup(uint64_t group) {
+  if (group == 0) return;
+  std::lock_guard<std::mutex> g(wb_mu_);
+  auto it = groups_.find(group);
+  if (it == groups_.end()) return;
+  if (it->second.outstanding == 0 && it->second.err.ok()) {
+    groups_.erase(it);
+  } else {
+    it->second.closed = true;  // erased by the worker that writes its last blob
+  }
+}
+
+void FileStore::SetWriteBehindLimit(uint64_t bytes) {
+  std::lock_guard<std::mutex> g(wb_mu_);
+  wb_limit_ = std::max<uint64_t>(1, bytes);
+}
+
+void FileStore::Attach(Pending& p, uint64_t group) {
+  if (std::find(p.groups.begin(), p.groups.end(), group) != p.groups.end()) return;
+  p.groups.push_back(group);
+  groups_[group].outstanding++;
+}
+
+Status FileStore::PutBlob(const Ref& ref, const Blob& b, bool* added, uint64_t group) {
   if (added) *added = false;
-  if (wb_pending_.count(ref)) return Status::Ok();
+  std::unique_lock<std::mutex> g(wb_mu_);
+  if (!groups_.count(group)) return Status::Err(BSG_EINVAL, "unknown write group");
+  auto it = wb_pending_.find(ref);
+  if (it != wb_pending_.end()) {  // queued by someone: this group waits for that write too
+    Attach(it->second, group);
+    return Status::Ok();
+  }
   if (wb_threads_.empty())
     for (int i = 0; i < kWriterThreads; ++i) wb_threads_.emplace_back([this] { Worker(); });
-  // bounded: wait for the writers when a GiB is pending
-  wb_done_cv_.wait(g, [&] { return wb_bytes_ < kWriteBehindBytes || !wb_err_.ok(); });
-  if (!wb_err_.ok()) return wb_err_;
-  wb_pending_.emplace(ref, b);
+  // bounded: wait for the writers while the limit's worth of bytes is pending
+  wb_done_cv_.wait(g, [&] { return wb_bytes_ < wb_limit_; });
+  // another caller may have queued the same blob while this one waited
+  it = wb_pending_.find(ref);
+  if (it != wb_pending_.end()) {
+    Attach(it->second, group);
+    return Status::Ok();
+  }
+  Pending& p = wb_pending_[ref];
+  p.blob = b;
+  Attach(p, group);
   wb_bytes_ += b.size;
-  wb_queue_.emplace_back(ref, b);
+  wb_queue_.push_back(ref);
   if (added) *added = true;
   g.unlock();
   wb_cv_.notify_one();
@@ -136,30 +183,51 @@ Status FileStore::PutBlob(const Ref& ref, const Blob& b, bool* added) {
 
 void FileStore::Worker() {
   for (;;) {
-    std::pair<Ref, Blob> job;
+    Ref ref;
+    Blob blob;
     {
       std::unique_lock<std::mutex> g(wb_mu_);
       wb_cv_.wait(g, [&] { return wb_stop_ || !wb_queue_.empty(); });
       if (wb_queue_.empty()) return;  // stopping
-      job = std::move(wb_queue_.front());
+      ref = wb_queue_.front();
       wb_queue_.pop_front();
+      blob = wb_pending_.at(ref).blob;  // the entry stays (Get serves it) until written
     }
     bool added = false;
-    Status s = PutWithRef(job.first, job.second.bytes(), job.second.size, &added);
+    Status s = PutWithRef(ref, blob.bytes(), blob.size, &added);
     {
       std::lock_guard<std::mutex> g(wb_mu_);
-      if (!s.ok() && wb_err_.ok()) wb_err_ = s;
-      wb_pending_.erase(job.first);
-      wb_bytes_ -= job.second.size;
+      auto it = wb_pending_.find(ref);
+      for (uint64_t id : it->second.groups) {
+        Group& gr = groups_[id];
+        if (!s.ok() && gr.err.ok()) gr.err = s;
+        if (--gr.outstanding == 0 && gr.closed && gr.err.ok()) groups_.erase(id);
+      }
+      wb_pending_.erase(it);
+      wb_bytes_ -= blob.size;
     }
     wb_done_cv_.notify_all();
   }
 }
 
-Status FileStore::Flush() {
+Status FileStore::Flush(uint64_t group) {
   std::unique_lock<std::mutex> g(wb_mu_);
-  wb_done_cv_.wait(g, [&] { return wb_pending_.empty(); });
-  return wb_err_;
+  auto it = groups_.find(group);
+  if (it == groups_.end()) return Status::Err(BSG_EINVAL, "unknown write group");
+  wb_done_cv_.wait(g, [&] { return groups_[group].outstanding == 0; });
+  Group& gr = groups_[group];
+  Status s = gr.err;
+  gr.err = Status::Ok();  // reported once
+  if (gr.closed && group != 0) groups_.erase(group);
+  return s;
+}
+
+Status FileStore::FlushAll() {
+  {
+    std::unique_lock<std::mutex> g(wb_mu_);
+    wb_done_cv_.wait(g, [&] { return wb_pending_.empty(); });
+  }
+  return Flush(0);
 }
 
 Status FileStore::GetBlob(const Ref& ref, Blob* out) {
@@ -167,7 +235,7 @@ Status FileStore::GetBlob(const Ref& ref, Blob* out) {
     std::lock_guard<std::mutex> g(wb_mu_);
     auto it = wb_pending_.find(ref);
     if (it != wb_pending_.end()) {
-      *out = it->second;
+      *out = it->second.blob;
       return Status::Ok();
     }
   }
@@ -179,7 +247,8 @@ Status FileStore::Get(const Ref& ref, std::vector<uint8_t>* out) {  // file.go:4
     std::lock_guard<std::mutex> g(wb_mu_);
     auto it = wb_pending_.find(ref);
     if (it != wb_pending_.end()) {  // accepted by PutBlob, not written yet
-      out->assign(it->second.bytes(), it->second.bytes() + it->second.size);
+      const Blob& b = it->second.blob;
+      out->assign(b.bytes(), b.bytes() + b.size);
       return Status::Ok();
     }
   }
@@ -244,7 +313,7 @@ Status FileStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool
 
 // file.go:79-154: walk blobs/<2>/<4>/<64> in name order, starting after `start`.
 Status FileStore::ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) {
-  Status s = Flush();  // blobs accepted by PutBlob are listed once written
+  Status s = FlushAll();  // blobs accepted by PutBlob are listed once written
   if (!s.ok()) return s;
   const std::string blobroot = root_ + "/blobs";
   s = mkdir_all(blobroot);

@@ -20,6 +20,7 @@
 #include <tuple>
 
 #include "../../include/bs_split.hpp"
+#include "host_pool.h"
 
 namespace bs {
 
@@ -143,11 +144,50 @@ Status MemStore::PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool*
   return Status::Ok();
 }
 
-Status MemStore::PutBlob(const Ref& ref, const Blob& b, bool* added) {  // mem.go:62-76
+Status MemStore::PutBlob(const Ref& ref, const Blob& b, bool* added, uint64_t) {  // mem.go:62-76
   std::lock_guard<std::mutex> g(mu_);
   const bool add = blobs_.emplace(ref, b).second;
+  if (add && b.base_size > b.size) {  // an alias into a larger buffer: account for its share
+    Share& sh = shares_[Owner(b.data)];
+    sh.base_size = b.base_size;
+    sh.live += b.size;
+    sh.refs.push_back(ref);
+  }
   if (added) *added = add;
   return Status::Ok();
+}
+
+// Copies the blobs still aliasing a sealed buffer into buffers of their own once they keep
+// less than half of it alive; the buffer is then freed with its last other reference.
+void MemStore::MaybeCompact(std::map<Owner, Share, std::owner_less<Owner>>::iterator it) {
+  Share& sh = it->second;
+  if (!sh.sealed || sh.live * 2 >= sh.base_size) return;
+  for (const Ref& r : sh.refs) {
+    auto b = blobs_.find(r);
+    if (b == blobs_.end()) continue;  // deleted
+    std::shared_ptr<uint8_t> own(new uint8_t[b->second.size ? b->second.size : 1],
+                                 std::default_delete<uint8_t[]>());
+    if (b->second.size) std::memcpy(own.get(), b->second.bytes(), b->second.size);
+    b->second = Blob{std::move(own), b->second.size, 0};
+  }
+  shares_.erase(it);
+}
+
+void MemStore::Seal(const Blob& whole) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = shares_.find(Owner(whole.data));
+  if (it == shares_.end()) return;
+  it->second.sealed = true;
+  MaybeCompact(it);
+}
+
+size_t MemStore::HeldBytes() const {
+  std::lock_guard<std::mutex> g(mu_);
+  size_t n = 0;
+  for (const auto& kv : blobs_)
+    if (kv.second.base_size <= kv.second.size) n += kv.second.size;
+  for (const auto& kv : shares_) n += kv.second.base_size;
+  return n;
 }
 
 Status MemStore::ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) {
@@ -165,7 +205,23 @@ Status MemStore::ListRefs(const Ref& start, const std::function<Status(const Ref
 
 Status MemStore::Delete(const Ref& ref) {  // mem.go:79-85
   std::lock_guard<std::mutex> g(mu_);
-  blobs_.erase(ref);
+  auto b = blobs_.find(ref);
+  if (b == blobs_.end()) return Status::Ok();
+  const Blob blob = b->second;
+  blobs_.erase(b);
+  if (blob.base_size > blob.size) {
+    auto it = shares_.find(Owner(blob.data));
+    if (it != shares_.end()) {
+      Share& sh = it->second;
+      sh.live -= blob.size;
+      sh.refs.erase(std::find(sh.refs.begin(), sh.refs.end(), ref));
+      if (sh.refs.empty()) {
+        shares_.erase(it);
+      } else {
+        MaybeCompact(it);
+      }
+    }
+  }
   return Status::Ok();
 }
 
@@ -356,6 +412,7 @@ std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) 
   std::unique_ptr<Writer> w(new Writer(opt.device));
   w->st_ = st;
   w->rp_ = dynamic_cast<RefPutter*>(st);
+  if (w->rp_) w->group_ = w->rp_->OpenGroup();
   w->opt_ = opt;
   if (w->opt_.fanout == 0) w->opt_.fanout = 1;
   bsg_params p;
@@ -374,6 +431,7 @@ std::unique_ptr<Writer> Writer::New(Store* st, const Options& opt, Status* err) 
 }
 
 Writer::~Writer() {
+  if (rp_) rp_->CloseGroup(group_);
   if (ctx_)
     ctx_release(CtxKey{opt_.device, opt_.bits, (uint32_t)std::max(opt_.min_size, 0), opt_.tile},
                 ctx_);
@@ -392,6 +450,13 @@ Status Writer::PutProto(const Node& node, Ref* ref) {
 
 Status Writer::PutProtos(const std::vector<const Node*>& nodes, std::vector<Ref>* refs) {
   refs->assign(nodes.size(), Ref{});
+  if (nodes.empty()) return Status::Ok();
+  // A node is stored only once everything under it is (split/split.go:71-77 Puts a node's
+  // chunks before PutProto of the node): wait for this Writer's write-behind blobs first.
+  if (rp_) {
+    Status f = rp_->Flush(group_);
+    if (!f.ok()) return f;
+  }
   if (!rp_) {  // the store hashes each blob itself
     for (size_t i = 0; i < nodes.size(); ++i) {
       Status s = PutProto(*nodes[i], &(*refs)[i]);
@@ -481,6 +546,7 @@ Status Writer::Drain() {
     while (skip >= pieces_[k].size) skip -= pieces_[k++].size;
     if (skip + c.len <= pieces_[k].size) {
       blob.data = std::shared_ptr<const uint8_t>(pieces_[k].buf, pieces_[k].buf.get() + skip);
+      blob.base_size = pieces_[k].size;
     } else {
       std::shared_ptr<uint8_t> own(new uint8_t[c.len], std::default_delete<uint8_t[]>());
       uint64_t done = 0;
@@ -494,12 +560,13 @@ Status Writer::Drain() {
     Ref ref;
     std::memcpy(ref.data(), c.ref, 32);
     bool added;
-    Status s = rp_ ? rp_->PutBlob(ref, blob, &added)                // GPU ref, no re-hash
+    Status s = rp_ ? rp_->PutBlob(ref, blob, &added, group_)        // GPU ref, no re-hash
                    : st_->Put(blob.bytes(), c.len, &ref, &added);  // store computes the ref
     if (!s.ok()) return s;
     emitted_ += c.len;
     while (!pieces_.empty() && base_ + pieces_.front().size <= emitted_) {  // fully emitted
       base_ += pieces_.front().size;
+      if (rp_) rp_->Seal(Blob{pieces_.front().buf, pieces_.front().size, 0});
       pieces_.pop_front();
     }
     s = Add(ref, c.len, c.level / opt_.fanout);  // split/split.go:86
@@ -526,21 +593,10 @@ static std::shared_ptr<uint8_t> alloc_piece(size_t n) {
                                   std::default_delete<uint8_t[]>());
 }
 
-// Host threads for a large Write's copies (as bsg_write's own: BSG_COPY_THREADS, default 8).
-static unsigned writer_threads() {
-  static unsigned v = 0;
-  if (!v) {
-    const char* e = std::getenv("BSG_COPY_THREADS");
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    v = std::max(1u, std::min(hw, e ? (unsigned)std::max(1, std::atoi(e)) : 8u));
-  }
-  return v;
-}
-
 // Copies p[0..n) into dst (the Writer's piece) and, through the zero-copy window, into the
 // context's pinned staging: one read of the caller's bytes feeds both copies (each thread
 // copies a 64 KiB slice into the piece, then from there, still in cache, into the window), on
-// up to writer_threads() threads for large Writes.
+// the process-wide copy pool (host_pool.h: BSG_COPY_THREADS threads shared by all Writers).
 Status Writer::Copy(const uint8_t* p, size_t n, uint8_t* dst) {
   size_t done = 0;
   while (done < n) {
@@ -560,18 +616,13 @@ Status Writer::Copy(const uint8_t* p, size_t n, uint8_t* dst) {
       }
     };
     constexpr size_t kPerThread = 2ull << 20;
-    const unsigned nt = (unsigned)std::min<size_t>(writer_threads(), k / kPerThread);
+    const size_t nt = std::min<size_t>((size_t)bsg::copy_threads(), k / kPerThread);
     if (nt <= 1) {
       work(0, k);
     } else {
-      std::vector<std::thread> th;
       const size_t per = ((k + nt - 1) / nt + 4095) & ~(size_t)4095;
-      for (unsigned t = 0; t < nt; ++t) {
-        const size_t lo = t * per;
-        if (lo >= k) break;
-        th.emplace_back(work, lo, std::min(k, lo + per));
-      }
-      for (auto& x : th) x.join();
+      bsg::parallel_for((k + per - 1) / per,
+                        [&](size_t t) { work(t * per, std::min(k, t * per + per)); });
     }
     rc = bsg_write_commit(ctx_, k);
     if (rc) return Status::Err(rc, std::string("bsg_write_commit: ") + bsg_errstr(rc));
@@ -634,10 +685,11 @@ Status Writer::Close() {  // split/split.go:104-126
       }
     }
   }
+  // the root last, once every blob and node under it is stored (write-behind stores)
+  if (rp_ && !(s = rp_->Flush(group_)).ok()) return sticky_ = s;
   s = PutProto(root->node, &root_);
   if (!s.ok()) return sticky_ = s;
   levels_.clear();
-  if (rp_ && !(s = rp_->Flush()).ok()) return sticky_ = s;  // write-behind stores
   return Status::Ok();
 }
 
@@ -757,13 +809,7 @@ Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint
       }
     }
   };
-  if (errs.size() == 1) {
-    fetch(0);
-  } else {
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < errs.size(); ++t) th.emplace_back(fetch, t);
-    for (std::thread& x : th) x.join();
-  }
+  bsg::parallel_for(errs.size(), fetch);
   for (const Status& e : errs)
     if (!e.ok()) {
       w.st = e;
@@ -799,14 +845,19 @@ Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint
 // window is taken, the one after it is started in the background.
 Status Reader::TakeLeaf() {
   const uint64_t at = stack_.back().offset;
-  auto take = [&](Window&& w) -> Status {
+  // Sequential reading (the first leaf node, or the one right after the last taken) verifies
+  // whole windows and reads ahead; a read elsewhere (a seek) verifies just its leaf node, so a
+  // random or backward read costs one leaf node's fetch and hash, not a 256 MiB window.
+  const bool sequential = at == next_leaf_;
+  next_leaf_ = at + stack_.back().size;
+  auto take = [&](Window&& w, bool ahead) -> Status {
     if (!w.st.ok()) {
       window_.clear();
       if (std::find(w.covered.begin(), w.covered.end(), at) != w.covered.end()) return w.st;
       return Status::Ok();  // a failure further on, in a window this read does not need
     }
     window_ = std::move(w.leaves);
-    if (!w.end)
+    if (!w.end && ahead)
       ahead_ = std::async(std::launch::async,
                           [this, cur = std::move(w.cursor)]() mutable {
                             return VerifyRun(std::move(cur), nullptr, window_bytes_);
@@ -814,14 +865,16 @@ Status Reader::TakeLeaf() {
     return Status::Ok();
   };
   auto it = window_.find(at);
-  if (it == window_.end() && ahead_.valid()) {
-    Status s = take(ahead_.get());
+  if (it == window_.end() && sequential && ahead_.valid()) {
+    Status s = take(ahead_.get(), true);
     if (!s.ok()) return s;
     it = window_.find(at);
   }
   if (it == window_.end()) {
-    if (ahead_.valid()) ahead_.wait();  // a window for elsewhere in the stream: dropped
-    ahead_ = std::future<Window>();
+    if (sequential) {  // a window read ahead for elsewhere in the stream: dropped
+      if (ahead_.valid()) ahead_.wait();
+      ahead_ = std::future<Window>();
+    }
     if (!hasher_) hasher_.reset(new GpuHasher(device_));
     // the walk, positioned after stack_.back(): each internal node on the path and its child
     // after the one on the path
@@ -833,9 +886,9 @@ Status Reader::TakeLeaf() {
       while (c < parent.nodes.size() && parent.nodes[c].offset <= on_path) ++c;
       cur.push_back(Frame{parent, c});
     }
-    Window w = VerifyRun(std::move(cur), &stack_.back(), window_bytes_);
+    Window w = VerifyRun(std::move(cur), &stack_.back(), sequential ? window_bytes_ : 0);
     if (!w.st.ok()) return w.st;
-    Status s = take(std::move(w));
+    Status s = take(std::move(w), sequential);
     if (!s.ok()) return s;
     it = window_.find(at);
     if (it == window_.end()) return Status::Err(kCorrupt, "tree node offsets repeat");
@@ -975,6 +1028,15 @@ size_t bsg_store_count(const bsg_store* s) {
   s->st->ListRefs(bs::Zero, [&](const bs::Ref&) { ++k; return bs::Status::Ok(); });
   return k;
 }
+
+int bsg_filestore_set_write_behind(bsg_store* s, uint64_t bytes) {
+  auto* fs = s ? dynamic_cast<bs::FileStore*>(s->st.get()) : nullptr;
+  if (!fs || !bytes) return BSG_EINVAL;
+  fs->SetWriteBehindLimit(bytes);
+  return BSG_OK;
+}
+
+size_t bsg_store_held_bytes(const bsg_store* s) { return s && s->mem ? s->mem->HeldBytes() : 0; }
 
 int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n) {
   if (!s || !ref || !n) return BSG_EINVAL;

@@ -10,10 +10,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -23,6 +27,7 @@
 #include "bsgpu_internal.h"
 #include "bsgpu_launch.h"
 #include "buzhash32_table.inc"
+#include "host_pool.h"
 
 using namespace bsg;
 
@@ -106,12 +111,11 @@ int herr(hipError_t e) { return e == hipSuccess ? BSG_OK : BSG_EDEVICE; }
 
 // BSG_DEBUG_SYNC=1: synchronise and report after every launch (debugging hangs/faults)
 bool debug_sync() {
-  static int v = -1;
-  if (v < 0) {
+  static const bool v = [] {
     const char* e = std::getenv("BSG_DEBUG_SYNC");
-    v = (e && *e == '1') ? 1 : 0;
-  }
-  return v == 1;
+    return e && *e == '1';
+  }();
+  return v;
 }
 hipError_t dbg(const char* what, hipStream_t s, hipError_t e) {
   if (!debug_sync() || e != hipSuccess) return e;
@@ -121,6 +125,14 @@ hipError_t dbg(const char* what, hipStream_t s, hipError_t e) {
   std::fprintf(stderr, " %s\n", hipGetErrorString(e));
   std::fflush(stderr);
   return e;
+}
+
+// Polls of a k_sha helper-wave handshake before it gives up and flags a device error (~1 s).
+// BSG_DEBUG_SEQ_WAIT=<n> overrides it (read at every run): 0 makes every handshake fail at once,
+// which is how the tests drive the device-error path (Counters::error -> BSG_EDEVICE).
+uint32_t seq_wait_limit() {
+  const char* e = std::getenv("BSG_DEBUG_SEQ_WAIT");
+  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 24);
 }
 
 int long_mode() {  // BSG_LONG_MODE = off | all (experiments); default auto
@@ -338,7 +350,7 @@ struct bsg_engine {
                buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
                jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
                data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
-               long_mode(), 4u * (uint32_t)num_cus};
+               long_mode(), 4u * (uint32_t)num_cus, seq_wait_limit()};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
@@ -398,7 +410,7 @@ struct bsg_engine {
                buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
                jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
                data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
-               long_mode(), 4u * (uint32_t)num_cus};
+               long_mode(), 4u * (uint32_t)num_cus, seq_wait_limit()};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
@@ -456,15 +468,99 @@ struct bsg_engine {
 // tile i+1 waits for tile i's k_sha and continues from the exported midstate.
 // Records complete in tile order; bsg_pending/bsg_drain hand them out in stream order.
 // ------------------------------------------------------------------------------------------
+namespace bsg {
+
 // Host threads copying a large Write into pinned staging (BSG_COPY_THREADS, default 8).
 int copy_threads() {
-  static int v = -1;
-  if (v < 0) {
+  static const int v = [] {
     const char* e = std::getenv("BSG_COPY_THREADS");
-    v = e ? std::max(1, std::min(64, std::atoi(e))) : 8;
-  }
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    return std::max(1, std::min(hw, e ? std::min(64, std::atoi(e)) : 8));
+  }();
   return v;
 }
+
+namespace {
+// One parallel_for call: workers and the caller take indices from `next` until none are left.
+struct PoolJob {
+  const std::function<void(size_t)>* fn = nullptr;
+  size_t n = 0;
+  std::atomic<size_t> next{0}, done{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  void run() {
+    for (size_t i; (i = next.fetch_add(1)) < n;) {
+      (*fn)(i);
+      if (done.fetch_add(1) + 1 == n) {
+        std::lock_guard<std::mutex> g(mu);
+        cv.notify_all();
+      }
+    }
+  }
+};
+
+class CopyPool {
+ public:
+  explicit CopyPool(int workers) {
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { Work(); });
+  }
+  void Run(size_t n, const std::function<void(size_t)>& fn) {
+    auto job = std::make_shared<PoolJob>();
+    job->fn = &fn;
+    job->n = n;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(job);
+    }
+    cv_.notify_all();
+    job->run();  // the caller works too
+    {
+      std::unique_lock<std::mutex> g(job->mu);
+      job->cv.wait(g, [&] { return job->done.load() == job->n; });
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = q_.begin(); it != q_.end(); ++it)
+      if (*it == job) {
+        q_.erase(it);
+        break;
+      }
+  }
+
+ private:
+  void Work() {
+    for (;;) {
+      std::shared_ptr<PoolJob> job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !q_.empty(); });
+        job = q_.front();
+        if (job->next.load() >= job->n) {  // every index taken: nothing left to help with
+          q_.pop_front();
+          continue;
+        }
+      }
+      job->run();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::shared_ptr<PoolJob>> q_;
+  std::vector<std::thread> th_;
+};
+}  // namespace
+
+void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
+  if (n == 0) return;
+  if (n == 1 || copy_threads() <= 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  // never destroyed: its workers stay blocked on the queue until the process exits
+  static CopyPool* pool = new CopyPool(copy_threads() - 1);
+  pool->Run(n, fn);
+}
+
+}  // namespace bsg
 
 constexpr int kMaxSlots = 8;
 constexpr uint64_t kDefaultCarryCap = 8ull << 20;
@@ -799,29 +895,31 @@ struct bsg_ctx {
 
   static void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
     constexpr size_t kPiece = 2ull << 20;  // per thread, at least
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const unsigned nt = (unsigned)std::min<size_t>({(size_t)copy_threads(), (size_t)hw, n / kPiece});
+    const size_t nt = std::min<size_t>((size_t)copy_threads(), n / kPiece);
     if (nt <= 1) {
       std::memcpy(dst, src, n);
       return;
     }
-    std::vector<std::thread> th;
-    const size_t per = (n + nt - 1) / nt;
-    for (unsigned k = 0; k < nt; ++k) {
+    const size_t per = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
+    parallel_for((n + per - 1) / per, [=](size_t k) {
       const size_t o = k * per;
-      if (o >= n) break;
-      th.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(per, n - o)); });
-    }
-    for (auto& x : th) x.join();
+      std::memcpy(dst + o, src + o, std::min(per, n - o));
+    });
   }
 
-  // Start a new stream on the same buffers (bsg_reset): everything in flight is finished first.
+  // Start a new stream on the same buffers (bsg_reset): everything in flight is waited for and
+  // discarded, also after a device error (Counters::error is per run: the buffers stay valid).
+  // Only a failing HIP call (a real fault) leaves the context unusable: bsg_free it.
   int reset() {
-    while (!inflight.empty()) {
-      bool got = false;
-      int rc = collect_front(true, &got);
-      if (rc) return rc;
+    for (int k = 0; k < nslots; ++k) {
+      TileSlot& t = slots[k];
+      if (t.eng) HCHECK(hipStreamSynchronize(t.eng->stream));
+      if (t.h2d_ev) HCHECK(hipEventSynchronize(t.h2d_ev));
+      t.busy = false;
+      t.sel_read = t.recs_enq = false;
+      if (t.eng) t.eng->enqueued = false;
     }
+    inflight.clear();
     ready.clear();
     cur = 0;
     fill = 0;
@@ -1353,9 +1451,7 @@ static void par_gather(uint8_t* dst, const uint8_t* src, const uint64_t* so,
                        const uint8_t* const* sp, const uint64_t* sl, const uint64_t* dofs,
                        uint32_t n, uint64_t total) {
   constexpr uint64_t kPiece = 2ull << 20;  // per thread, at least
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const unsigned nt = (unsigned)std::min<uint64_t>({(uint64_t)copy_threads(), (uint64_t)hw,
-                                                    total / kPiece});
+  const uint64_t nt = std::min<uint64_t>((uint64_t)copy_threads(), total / kPiece);
   auto run = [=](uint32_t a, uint32_t b) {
     for (uint32_t k = a; k < b; ++k)
       if (sl[k]) std::memcpy(dst + dofs[k], sp ? sp[k] : src + so[k], sl[k]);
@@ -1364,19 +1460,19 @@ static void par_gather(uint8_t* dst, const uint8_t* src, const uint64_t* so,
     run(0, n);
     return;
   }
-  std::vector<std::thread> th;
+  std::vector<std::pair<uint32_t, uint32_t>> runs;
   const uint64_t per = (total + nt - 1) / nt;
   uint32_t a = 0;
   uint64_t acc = 0;
   for (uint32_t k = 0; k < n; ++k) {
     acc += sl[k];
     if (acc >= per || k + 1 == n) {
-      th.emplace_back(run, a, k + 1);
+      runs.emplace_back(a, k + 1);
       a = k + 1;
       acc = 0;
     }
   }
-  for (auto& x : th) x.join();
+  parallel_for(runs.size(), [&](size_t i) { run(runs[i].first, runs[i].second); });
 }
 
 struct bsg_hasher {

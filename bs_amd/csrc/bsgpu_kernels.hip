@@ -1907,10 +1907,10 @@ __device__ __forceinline__ uint32_t lds_seq_load(uint32_t* p) {
 __device__ __forceinline__ void lds_seq_store(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // rows land first
 }
-// Waits until *p == want (wave-uniform). Bounded (~1 s); a timeout, never expected, flags a
-// device error so that the run fails instead of hanging.
+// Waits until *p == want (wave-uniform). Bounded (a.seq_wait_limit polls, ~1 s); a timeout,
+// never expected, flags a device error so that the run fails instead of hanging.
 __device__ bool lds_seq_wait(const ShaArgs& a, uint32_t* p, uint32_t want) {
-  for (uint32_t i = 0; i < (1u << 24); ++i) {
+  for (uint32_t i = 0; i < a.seq_wait_limit; ++i) {
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)lds_seq_load(p)) == want) return true;
     __builtin_amdgcn_s_sleep(1);
   }

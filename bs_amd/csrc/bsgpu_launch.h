@@ -93,6 +93,8 @@ struct ShaArgs {
   uint64_t span;            // bytes from data to the end of the last stream (regions)
   int long_mode;            // 0 auto, 1 per-lane only, 2 wave mode only (experiments)
   uint32_t waves;           // waves of the k_sha grid (4 per CU)
+  uint32_t seq_wait_limit;  // polls before a helper-wave handshake flags a device error
+                            // (~1 s; BSG_DEBUG_SEQ_WAIT overrides it, 0: fail at once, tests)
 };
 
 struct BlobShaArgs {

@@ -71,21 +71,40 @@ class Store {
 struct Blob {
   std::shared_ptr<const uint8_t> data;
   size_t size = 0;
+  // bytes of the buffer `data` aliases into when that buffer is larger than the blob (a Write
+  // piece); 0 when the blob owns exactly its bytes
+  size_t base_size = 0;
   const uint8_t* bytes() const { return data.get(); }
 };
 
+// Write groups: a store that writes behind (store/file) accepts a blob before it is durable.
+// Each caller (one split::Writer) opens a group, puts its blobs in it, and Flush(group) waits for
+// exactly the blobs that group put — including ones another group had already queued when this
+// one asked for them — and returns the first error among them (then forgets it). So one
+// Writer's failed write is reported to that Writer only, and a Writer can guarantee "a tree node
+// is stored only after every blob under it is" (split/split.go:71-77,118 store chunks before
+// their node) by flushing its group before it stores a node. Group 0 is the ungrouped caller.
 class RefPutter {
  public:
   virtual ~RefPutter() = default;
   virtual Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) = 0;
   // The same with shared ownership of the bytes: a store that retains blobs in memory keeps
   // the Blob itself (no copy); others just read it.
-  virtual Status PutBlob(const Ref& ref, const Blob& b, bool* added) {
+  virtual Status PutBlob(const Ref& ref, const Blob& b, bool* added, uint64_t group = 0) {
+    (void)group;
     return PutWithRef(ref, b.bytes(), b.size, added);
   }
-  // Waits for blobs a store accepted without writing them yet (write-behind) and returns the
-  // first error among them. split.Writer.Close calls it.
-  virtual Status Flush() { return Status::Ok(); }
+  virtual uint64_t OpenGroup() { return 0; }
+  virtual void CloseGroup(uint64_t group) { (void)group; }
+  // Waits for the group's accepted-but-unwritten blobs; the first error among them.
+  virtual Status Flush(uint64_t group) {
+    (void)group;
+    return Status::Ok();
+  }
+  // No more blobs aliasing `whole`'s buffer will be put (split::Writer: a Write piece whose
+  // bytes are all emitted as chunks). A store that keeps such aliases (store/mem) then keeps
+  // private copies of them instead, if they hold less than half of the buffer alive.
+  virtual void Seal(const Blob& whole) { (void)whole; }
 };
 
 // Batched/one-off SHA-256 of host bytes on the GPU (bsg_hasher: persistent device buffers +
@@ -118,15 +137,29 @@ class MemStore : public Store, public RefPutter {
   Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
   Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
   // Keeps b itself (mem.go:71 keeps the caller's slice): no copy of the chunk bytes.
-  Status PutBlob(const Ref& ref, const Blob& b, bool* added) override;
+  Status PutBlob(const Ref& ref, const Blob& b, bool* added, uint64_t group = 0) override;
+  void Seal(const Blob& whole) override;
   // bs.DeleterStore (store.go:50-54): removes ref if present; absent refs are not an error
-  // (mem.go:79-85).
+  // (mem.go:79-85). When the blobs left aliasing a sealed buffer hold less than half of it,
+  // they are copied out, so deleting most of a Write's chunks frees the Write's memory.
   Status Delete(const Ref& ref);
   size_t Size() const;
+  // Bytes of the buffers the store keeps alive (its own copies plus every aliased buffer
+  // once), for tests and diagnostics.
+  size_t HeldBytes() const;
 
  private:
+  // Blobs aliasing one larger buffer (keyed by the buffer's owner): how much of it is live.
+  struct Share {
+    size_t base_size = 0, live = 0;
+    bool sealed = false;
+    std::vector<Ref> refs;
+  };
+  using Owner = std::weak_ptr<const uint8_t>;
+  void MaybeCompact(std::map<Owner, Share, std::owner_less<Owner>>::iterator it);  // under mu_
   mutable std::mutex mu_;
   std::map<Ref, Blob> blobs_;
+  std::map<Owner, Share, std::owner_less<Owner>> shares_;
   GpuHasher hasher_;
 };
 
@@ -144,11 +177,18 @@ class FileStore : public Store, public RefPutter {
   Status ListRefs(const Ref& start, const std::function<Status(const Ref&)>& f) override;
   Status PutWithRef(const Ref& ref, const uint8_t* data, size_t n, bool* added) override;
   // Write-behind (split.Writer's chunks): the Blob is kept, and written by a pool of writer
-  // threads; Get sees it at once, Flush waits for the files. *added: not already pending.
-  Status PutBlob(const Ref& ref, const Blob& b, bool* added) override;
-  Status Flush() override;
+  // threads; Get sees it at once, Flush(group) waits for the group's files. *added: not already
+  // pending (a blob pending for another group is shared: this group's Flush waits for it too).
+  Status PutBlob(const Ref& ref, const Blob& b, bool* added, uint64_t group = 0) override;
+  uint64_t OpenGroup() override;
+  void CloseGroup(uint64_t group) override;
+  Status Flush(uint64_t group) override;
+  // Waits for every pending blob (ListRefs, the destructor); the ungrouped callers' first error.
+  Status FlushAll();
   std::string BlobPath(const Ref& ref) const;
   const std::string& Root() const { return root_; }
+  // At most this many bytes are pending before PutBlob waits (tests shrink it).
+  void SetWriteBehindLimit(uint64_t bytes);
 
  private:
   Status MkdirFor(const std::string& path);  // os.MkdirAll of the blob's directory, cached
@@ -157,15 +197,26 @@ class FileStore : public Store, public RefPutter {
   GpuHasher hasher_;
   std::mutex dir_mu_;
   std::vector<bool> dirs_made_ = std::vector<bool>(1 << 16);  // blobs/hh/hhhh made, by hhhh
+  struct Pending {
+    Blob blob;
+    std::vector<uint64_t> groups;  // every group whose Flush must wait for this write
+  };
+  struct Group {
+    uint64_t outstanding = 0;  // blobs of this group not yet written
+    Status err;                // first failed write of the group, until Flush reports it
+    bool closed = false;       // CloseGroup called: forget it once outstanding reaches 0
+  };
+  void Attach(Pending& p, uint64_t group);  // under wb_mu_
   std::mutex wb_mu_;
   std::condition_variable wb_cv_, wb_done_cv_;
-  std::deque<std::pair<Ref, Blob>> wb_queue_;
-  std::map<Ref, Blob> wb_pending_;  // accepted, not yet written
-  uint64_t wb_bytes_ = 0;           // bytes of wb_pending_ (bounded: kWriteBehindBytes)
-  Status wb_err_;
+  std::deque<Ref> wb_queue_;           // refs of wb_pending_ in arrival order
+  std::map<Ref, Pending> wb_pending_;  // accepted, not yet written
+  std::map<uint64_t, Group> groups_ = {{0, Group{}}};  // group 0: ungrouped callers
+  uint64_t next_group_ = 1;
+  uint64_t wb_bytes_ = 0;              // bytes of wb_pending_ (bounded: wb_limit_)
+  uint64_t wb_limit_ = 1ull << 30;
   bool wb_stop_ = false;
   std::vector<std::thread> wb_threads_;
-  static constexpr uint64_t kWriteBehindBytes = 1ull << 30;
   static constexpr int kWriterThreads = 8;
 };
 
@@ -222,6 +273,7 @@ class Writer {
 
   Store* st_ = nullptr;
   RefPutter* rp_ = nullptr;
+  uint64_t group_ = 0;  // this Writer's write group in rp_ (RefPutter::OpenGroup)
   Options opt_;
   bsg_ctx* ctx_ = nullptr;
   // Stream bytes not yet emitted as chunks, kept as the Write() pieces they arrived in: a
@@ -295,6 +347,7 @@ class Reader {
   bool verify_ = false;
   int device_ = 0;
   bool cache_valid_ = false;  // cache_ holds stack_.back()'s leaves
+  uint64_t next_leaf_ = 0;    // offset right after the last leaf node taken (verify mode)
   std::vector<Blob> cache_;   // verified chunks of that leaf node
   // verified chunks of the window's later leaf nodes, by leaf-node offset
   std::map<uint64_t, std::vector<Blob>> window_;

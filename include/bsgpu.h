@@ -198,6 +198,13 @@ bsg_store* bsg_memstore_new(int device);   /* store/mem  (store/mem/mem.go:17-12
 bsg_store* bsg_filestore_new(const char* root, int device);
 void bsg_store_free(bsg_store* s);
 size_t bsg_store_count(const bsg_store* s);
+/* store/file writes split.Writer's chunks behind (bs::FileStore::PutBlob): at most `bytes` of
+ * accepted, unwritten blobs are pending before a Put waits (default 1 GiB). BSG_EINVAL for
+ * store/mem. */
+int bsg_filestore_set_write_behind(bsg_store* s, uint64_t bytes);
+/* Bytes of host memory a store/mem keeps alive: its own blob copies plus, once each, the Write
+ * pieces its chunks alias (split.Writer hands chunks over without copying). 0 for store/file. */
+size_t bsg_store_held_bytes(const bsg_store* s);
 /* Get: copies min(cap, len) bytes, *n = blob length; returns BSG_ENOTFOUND if absent. */
 int bsg_store_get(bsg_store* s, const uint8_t ref[32], uint8_t* out, size_t cap, size_t* n);
 int bsg_store_put(bsg_store* s, const uint8_t* data, size_t n, uint8_t ref_out[32], int* added);

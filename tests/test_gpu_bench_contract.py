@@ -42,3 +42,23 @@ def test_bench_json_line():
     assert cb["kind"] in ("port", "reference") and cb["sample"]
     assert d["end_to_end"]["value"] > 0
     assert d["chain_roofline"]["frac"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_default_carries_configs2():
+    """The default workload (configs[1]) also carries the nested configs[2] record."""
+    cmd = [sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--configs2-steps", "1",
+           "--cpu-sample-mib", "64", "--e2e-mib", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["config"]["workload"].startswith("configs[1]")
+    c2 = d["configs2"]
+    assert c2["workload"].startswith("configs[2]") and c2["steps"] == 1
+    assert c2["value"] > d["value"] and c2["ms_per_step"] > 0
+    assert c2["roofline"]["kernel"] == "k_sha" and c2["roofline"]["frac"] > 0
+    assert c2["roofline"]["k_scan"]["frac"] > 0
+    assert c2["cpu_baseline"]["cores"] >= 1 and c2["cpu_baseline"]["full_writer"]["value"] > 0
+    assert set(c2["stage_ms"]) == set(d["stage_ms"])

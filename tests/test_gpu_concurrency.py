@@ -1,0 +1,196 @@
+"""The reference's threading contract, exercised on the GPU path through the C ABI.
+
+split.Writer is single-goroutine, but many Writers run at once (split/split.go:30-37; fs.Dir.AddDir
+opens one per file, fs/dir.go:157-174), and a store's Put is goroutine-safe (store/mem/mem.go:
+63-64). Here 8 host threads each drive their own split::Writer (mixed Bits / MinSize / Fanout,
+32 KiB and 32 MiB writes) into ONE shared store/mem, then ONE shared store/file with a small
+write-behind limit (duplicate chunks from different Writers race through its pending set), and
+then raw bsg_open/bsg_write contexts, Writers and verifying Readers all at once. The pooled
+streaming contexts, pooled hashers and the process-wide copy pool are shared by all of them.
+Every Root is checked against the C restatement of split.Writer (oracle bso_writer_root), every
+raw context's chunk list against the oracle split, every read back byte for byte.
+
+ctypes releases the GIL for the duration of each library call, so the threads really run the
+library concurrently.
+"""
+import os
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+# (seed, bytes, bits, min_size, fanout, write size). Seeds repeat on purpose: Writers 0/4 and
+# 2/6 write identical streams with identical params, so their chunks collide in the shared store.
+JOBS = [
+    (101, 24 * MiB + 7, 16, 1024, 8, 32 << 10),
+    (102, 40 * MiB, 13, 64, 4, 32 * MiB),
+    (103, 17 * MiB + 3, 12, 256, 2, 32 << 10),
+    (104, 33 * MiB, 20, 4096, 8, 32 * MiB),
+    (101, 24 * MiB + 7, 16, 1024, 8, 32 * MiB),
+    (105, 9 * MiB, 10, 17, 3, 32 << 10),
+    (103, 17 * MiB + 3, 12, 256, 2, 32 * MiB),
+    (106, 28 * MiB, 16, 1024, 8, 32 << 10),
+]
+
+
+@pytest.fixture(scope="module")
+def streams():
+    from bs_amd.synth import splitmix_array
+    return {seed: splitmix_array(seed, n) for seed, n, *_ in JOBS}
+
+
+@pytest.fixture(scope="module")
+def want_roots(oracle, table, streams):
+    """Root of every job from the C restatement of split.Writer, computed on 8 threads."""
+    def one(j):
+        seed, n, bits, ms, fo, _ = j
+        return oracle.writer_root(table, streams[seed], bits=bits, min_size=ms, fanout=fo)[0]
+    with ThreadPoolExecutor(8) as ex:
+        return list(ex.map(one, JOBS))
+
+
+def _write(gpu, st, data: np.ndarray, bits, ms, fo, piece, start: threading.Barrier | None):
+    w = gpu.Writer(st, bits=bits, min_size=ms, fanout=fo)
+    mv = memoryview(data)
+    if start is not None:
+        start.wait()
+    for i in range(0, len(data), piece):
+        w.write(mv[i:i + piece])
+    w.close()
+    root = w.root
+    w.free()
+    return root
+
+
+def _run_writers(gpu, st, streams):
+    start = threading.Barrier(len(JOBS))
+    with ThreadPoolExecutor(len(JOBS)) as ex:
+        futs = [ex.submit(_write, gpu, st, streams[seed], bits, ms, fo, piece, start)
+                for seed, n, bits, ms, fo, piece in JOBS]
+        return [f.result() for f in futs]
+
+
+def _reachable(st, root: bytes) -> set:
+    keep, todo = set(), [(root, True)]
+    while todo:
+        ref, traverse = todo.pop()
+        if ref in keep:
+            continue
+        keep.add(ref)
+        if traverse:
+            todo.extend(st.protect_children(ref))
+    return keep
+
+
+def test_eight_writers_one_memstore(gpu, streams, want_roots):
+    st = gpu.MemStore()
+    for rep in range(2):  # the second round runs on pooled contexts and hashers
+        roots = _run_writers(gpu, st, streams)
+        assert roots == want_roots, f"round {rep}"
+    # every blob any Writer stored is reachable from some Root, and every Root reads back
+    reach = set()
+    for r in roots:
+        reach |= _reachable(st, r)
+    assert reach == set(st.refs())
+    for (seed, *_), r in zip(JOBS, roots):
+        assert gpu.Reader(st, r).read_all() == streams[seed].tobytes()
+    st.free()
+
+
+def test_eight_writers_one_filestore(gpu, streams, want_roots, tmp_path):
+    st = gpu.FileStore(str(tmp_path / "fs"))
+    st.set_write_behind(1 * MiB)  # Puts wait for the writer threads all the time
+    roots = _run_writers(gpu, st, streams)
+    assert roots == want_roots
+    # the root is stored last: once Close returned, the whole tree is on disk
+    on_disk = set()
+    for dirpath, _, files in os.walk(str(tmp_path / "fs" / "blobs")):
+        on_disk |= {bytes.fromhex(f) for f in files}
+    reach = set()
+    for r in roots:
+        reach |= _reachable(st, r)
+    assert reach <= on_disk
+    assert set(st.refs()) == on_disk
+
+    # verifying Readers, concurrently, with small windows so that the background verification
+    # and the foreground one overlap across Readers
+    os.environ["BSG_VERIFY_WINDOW"] = str(4 * MiB)
+    try:
+        def read(i):
+            seed = JOBS[i][0]
+            return gpu.Reader(st, roots[i], verify=True).read_all() == streams[seed].tobytes()
+        with ThreadPoolExecutor(len(JOBS)) as ex:
+            assert all(ex.map(read, range(len(JOBS))))
+    finally:
+        del os.environ["BSG_VERIFY_WINDOW"]
+    st.free()
+
+
+def test_mixed_contexts_writers_readers(gpu, oracle, table, streams, want_roots):
+    """Raw streaming contexts (bsg_open / bsg_write / bsg_drain), Writers and verifying Readers
+    on 10 threads at the same time."""
+    st = gpu.MemStore()
+    base_roots = _run_writers(gpu, st, streams)  # something to read back concurrently
+    start = threading.Barrier(10)
+
+    def raw(seed, bits, ms, piece):
+        data = streams[seed]
+        sp = gpu.StreamingSplitter(bits=bits, min_size=ms)
+        start.wait()
+        recs = []
+        for i in range(0, len(data), piece):
+            sp.write(data[i:i + piece])
+            recs.append(sp.drain())
+        sp.close()
+        recs.append(sp.drain())
+        sp.free()
+        got = np.concatenate(recs)
+        ref = oracle.split(table, data, bits=bits, min_size=ms)
+        return (len(got) == len(ref) and (got["offset"] == ref["offset"]).all()
+                and (got["level"] == ref["level"]).all() and (got["ref"] == ref["ref"]).all())
+
+    def reader(i):
+        r = gpu.Reader(st, base_roots[i], verify=True)
+        start.wait()
+        out = r.read_all() == streams[JOBS[i][0]].tobytes()
+        r.free()
+        return out
+
+    def writer(i):
+        seed, n, bits, ms, fo, piece = JOBS[i]
+        return _write(gpu, st, streams[seed], bits, ms, fo, piece, start) == want_roots[i]
+
+    with ThreadPoolExecutor(10) as ex:
+        futs = [ex.submit(raw, 102, 13, 64, 7 * MiB + 5), ex.submit(raw, 104, 20, 4096, 1 * MiB),
+                ex.submit(raw, 105, 10, 17, 333_333), ex.submit(raw, 106, 16, 1024, 32 * MiB)]
+        futs += [ex.submit(writer, i) for i in (1, 3, 5, 7)]
+        futs += [ex.submit(reader, i) for i in (0, 2)]
+        assert [f.result() for f in futs] == [True] * 10
+    st.free()
+
+
+def test_concurrent_duplicate_puts_small_write_behind(gpu, tmp_path):
+    """store/file's write-behind under contention: 8 threads Put overlapping sets
+    of the same chunks through Writers writing identical streams while the pending limit is one
+    chunk; every Writer must report success, and each blob must exist exactly once, complete."""
+    from bs_amd.synth import splitmix_array
+    data = splitmix_array(77, 6 * MiB)
+    st = gpu.FileStore(str(tmp_path / "fs"))
+    st.set_write_behind(1)
+    start = threading.Barrier(8)
+    with ThreadPoolExecutor(8) as ex:
+        roots = list(ex.map(lambda k: _write(gpu, st, data, 12, 64, 4, (k + 1) * 65_536, start),
+                            range(8)))
+    assert len(set(roots)) == 1
+    refs = st.refs()
+    for ref in refs:
+        blob = st.get(ref)
+        import hashlib
+        assert hashlib.sha256(blob).digest() == ref
+    assert gpu.Reader(st, roots[0], verify=True).read_all() == data.tobytes()
+    st.free()

@@ -201,3 +201,32 @@ def test_writer_root_256mib_matches_c_writer(gpu, oracle, table, bits, min_size,
     want, _ = oracle.writer_root(table, data, bits=bits, min_size=min_size, fanout=fanout)
     assert root == want
     st.free()
+
+
+def test_memstore_does_not_keep_pieces_alive_for_few_chunks(gpu, oracle, table):
+    """store/mem keeps chunks as aliases of the Writer's Write piece (no copy, as mem.go:71
+    keeps the caller's slice). A piece must not stay alive for a few chunks: a second stream
+    whose chunks are almost all duplicates, or deleting most of a stream's chunks (gc), releases
+    it (the survivors are copied out)."""
+    from bs_amd.synth import splitmix_array
+    MiB = 1 << 20
+    a = splitmix_array(31, 48 * MiB)
+    st = gpu.MemStore()
+    _, root_a = write_all(gpu, memoryview(a), piece=len(a), st=st)
+    held1 = st.held_bytes()
+    assert len(a) <= held1 < len(a) + 2 * MiB
+    b = a.copy()
+    b[1000:1010] ^= 0xFF  # only the first chunk differs
+    _, root_b = write_all(gpu, memoryview(b), piece=len(b), st=st)
+    assert st.held_bytes() < held1 + 2 * MiB  # b's piece is not held for its one new chunk
+    assert gpu.Reader(st, root_b).read_all() == b.tobytes()
+    # gc-style deletion of 90 % of a's chunks (never b's first one)
+    ch = oracle.split(table, a)
+    doomed = [bytes(c["ref"]) for c in ch[1:]][: int(len(ch) * 0.9)]
+    for r in doomed:
+        st.delete(r)
+    assert st.held_bytes() < 0.2 * len(a)
+    keep = {bytes(c["ref"]) for c in ch} - set(doomed)
+    for r in keep:
+        assert len(st.get(r)) > 0
+    st.free()
