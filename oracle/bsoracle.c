@@ -614,6 +614,15 @@ static void tb_add(wstate* w, const uint8_t ref[32], uint64_t len, unsigned leve
 
 size_t bso_writer_root(const uint32_t table[256], const uint8_t* x, size_t n, unsigned split_bits,
                        unsigned min_size, unsigned fanout, int keep_copies, uint8_t root[32]) {
+    return bso_writer_root_fold(table, x, n, split_bits, min_size, fanout, keep_copies, 0, root);
+}
+
+/* fold_mode selects the recalled TreeBuilder.Root detail: 0 folds every
+ * non-empty level below the top (the library's choice); 1 folds only when the leaf level holds
+ * chunks (not when the last chunk itself closed a level). */
+size_t bso_writer_root_fold(const uint32_t table[256], const uint8_t* x, size_t n,
+                            unsigned split_bits, unsigned min_size, unsigned fanout,
+                            int keep_copies, int fold_mode, uint8_t root[32]) {
     wstate w;
     memset(&w, 0, sizeof w);
     w.keep = keep_copies;
@@ -636,7 +645,8 @@ size_t bso_writer_root(const uint32_t table[256], const uint8_t* x, size_t n, un
     size_t puts = w.nblobs;
     if (w.nlv) {
         /* TreeBuilder.Root: fold every non-empty level below the top into its parent */
-        for (size_t i = 0; i + 1 < w.nlv; i++) {
+        const int fold = fold_mode == 0 || w.lv[0].nc > 0;
+        for (size_t i = 0; fold && i + 1 < w.nlv; i++) {
             tbnode* t = &w.lv[i];
             if (!t->nc && !t->nn) continue;
             wnode* f = tb_F(&w, t);

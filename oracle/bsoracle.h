@@ -72,6 +72,9 @@ size_t bso_split_streams(const uint32_t table[256], const uint8_t* base, const u
  * (Go-unpinned), the same as oracle.py's py_tree_root. */
 size_t bso_writer_root(const uint32_t table[256], const uint8_t* x, size_t n, unsigned split_bits,
                        unsigned min_size, unsigned fanout, int keep_copies, uint8_t root[32]);
+size_t bso_writer_root_fold(const uint32_t table[256], const uint8_t* x, size_t n,
+                            unsigned split_bits, unsigned min_size, unsigned fanout,
+                            int keep_copies, int fold_mode, uint8_t root[32]);
 
 #ifdef __cplusplus
 }

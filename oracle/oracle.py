@@ -75,6 +75,10 @@ def lib():
         L.bso_writer_root.restype = ctypes.c_size_t
         L.bso_writer_root.argtypes = [u32p, u8p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint,
                                       ctypes.c_uint, ctypes.c_int, u8p]
+        L.bso_writer_root_fold.restype = ctypes.c_size_t
+        L.bso_writer_root_fold.argtypes = [u32p, u8p, ctypes.c_size_t, ctypes.c_uint,
+                                           ctypes.c_uint, ctypes.c_uint, ctypes.c_int,
+                                           ctypes.c_int, u8p]
         _lib = L
     return _lib
 
@@ -159,15 +163,18 @@ def split_streams(table: np.ndarray, base: np.ndarray, off, lens, bits: int = 16
 
 
 def writer_root(table: np.ndarray, data, bits: int = 16, min_size: int = 1024, fanout: int = 8,
-                keep_copies: bool = False) -> tuple[bytes, int]:
+                keep_copies: bool = False, fold: str = "nonempty") -> tuple[bytes, int]:
     """split.Writer end to end in C (Splitter + TreeBuilder + PutProto + Close): (Root, puts).
-    keep_copies also copies every blob as store/mem's Put would (puts counts them)."""
+    keep_copies also copies every blob as store/mem's Put would (puts counts them). fold: the
+    TreeBuilder.Root variant (py_tree_root)."""
     x = data if isinstance(data, np.ndarray) else np.frombuffer(bytes(data), dtype=np.uint8)
     x = np.ascontiguousarray(x, dtype=np.uint8)
     t = np.ascontiguousarray(table, dtype=np.uint32)
     root = np.zeros(32, dtype=np.uint8)
-    puts = lib().bso_writer_root(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x), bits,
-                                 min_size, fanout, int(keep_copies), _p(root, ctypes.c_uint8))
+    mode = {"nonempty": 0, "leaf_gated": 1}[fold]
+    puts = lib().bso_writer_root_fold(_p(t, ctypes.c_uint32), _p(x, ctypes.c_uint8), len(x),
+                                      bits, min_size, fanout, int(keep_copies), mode,
+                                      _p(root, ctypes.c_uint8))
     return root.tobytes(), int(puts)
 
 
@@ -292,10 +299,19 @@ class _Wrapped:  # split.nodeWrapper: a finished Node (its children already stor
         return proto_node(self.nodes, self.leaves, self.offset, self.size)
 
 
-def py_tree_root(chunks, fanout: int = 8, store: dict | None = None) -> bytes:
+def py_tree_root(chunks, fanout: int = 8, store: dict | None = None,
+                 fold: str = "nonempty") -> bytes:
     """chunks: iterable of (chunk_bytes, level) in stream order; returns Writer.Root (32 bytes).
     Chunk refs are SHA-256 of their bytes (bs.go:24-26). If `store` is given (a dict), every
-    Put lands in it (ref -> blob), like store/mem."""
+    Put lands in it (ref -> blob), like store/mem.
+
+    fold selects the one recalled detail of hashsplit's TreeBuilder.Root that changes Root
+    (DESIGN §2): "nonempty" (the library's choice, and the C oracle's) folds every non-empty
+    level below the top into its parent; "leaf_gated" folds the levels only when the leaf level
+    holds chunks, i.e. not when the last chunk itself closed a level (then any nodes waiting in
+    the levels between are not under the Root). The two differ only when the last chunk closes
+    a level while a level between it and the top is non-empty (tests/golden/tree_root_variants.json)."""
+    assert fold in ("nonempty", "leaf_gated")
     store = {} if store is None else store
 
     def put(b: bytes) -> bytes:
@@ -332,9 +348,10 @@ def py_tree_root(chunks, fanout: int = 8, store: dict | None = None) -> bytes:
     if not levels:
         return bytes(32)  # Root stays bs.Zero (split_test.go:15-25)
     # Root(): fold every non-empty level below the top into its parent
-    for i in range(len(levels) - 1):
-        if levels[i].chunks or levels[i].nodes:
-            levels[i + 1].nodes.append(F(levels[i]))
+    if fold == "nonempty" or levels[0].chunks:
+        for i in range(len(levels) - 1):
+            if levels[i].chunks or levels[i].nodes:
+                levels[i + 1].nodes.append(F(levels[i]))
     if len(levels) == 1:
         root = F(levels[0])
     else:

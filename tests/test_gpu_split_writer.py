@@ -230,3 +230,15 @@ def test_memstore_does_not_keep_pieces_alive_for_few_chunks(gpu, oracle, table):
     for r in keep:
         assert len(st.get(r)) > 0
     st.free()
+
+
+def test_writer_root_on_tree_fold_fixture(gpu):
+    """The library's Writer takes the "nonempty" TreeBuilder.Root variant on every case of
+    tests/golden/tree_root_variants.json (the streams where the recalled fold detail matters)."""
+    from bs_amd.synth import splitmix_array
+    from conftest import load_json
+    for c in load_json("tree_root_variants.json")["cases"]:
+        data = splitmix_array(c["seed"], c["length"])
+        _, root = write_all(gpu, memoryview(data), piece=32 * 1024, bits=c["bits"],
+                            min_size=c["min_size"], fanout=c["fanout"])
+        assert root.hex() == c["root_nonempty"], c["name"]

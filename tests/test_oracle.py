@@ -205,3 +205,30 @@ def test_c_writer_root_empty_and_synthetic(oracle, table):
             [(data[int(c["offset"]):int(c["offset"] + c["len"])], int(c["level"])) for c in ch],
             fanout)
         assert oracle.writer_root(table, data, bits=bits, min_size=64, fanout=fanout)[0] == want
+
+
+def test_tree_root_variant_fixture(oracle, table):
+    """tests/golden/tree_root_variants.json (make_tree_fixture.py): the Roots of both
+    TreeBuilder.Root fold variants, regenerated by the C oracle and the Python tree restatement;
+    the variants differ exactly on the cases marked so (the stream's last chunk closes a level
+    below a taller tree)."""
+    from bs_amd.synth import splitmix_array
+    from conftest import load_json
+    doc = load_json("tree_root_variants.json")
+    assert doc["library_variant"] == "nonempty"
+    assert any(c["variants_differ"] for c in doc["cases"])
+    assert any(not c["variants_differ"] for c in doc["cases"])
+    for c in doc["cases"]:
+        data = splitmix_array(c["seed"], c["length"])
+        kw = dict(bits=c["bits"], min_size=c["min_size"], fanout=c["fanout"])
+        ch = oracle.split(table, data, bits=c["bits"], min_size=c["min_size"])
+        assert len(ch) == c["chunks"] and int(ch["level"][-1]) == c["last_chunk_level"]
+        assert int(ch["offset"][-1] + ch["len"][-1]) == len(data)
+        for fold in ("nonempty", "leaf_gated"):
+            want = c["root_" + fold]
+            assert oracle.writer_root(table, data, fold=fold, **kw)[0].hex() == want
+            if len(ch) < 500:
+                pieces = [(data[int(x["offset"]):int(x["offset"] + x["len"])], int(x["level"]))
+                          for x in ch]
+                assert oracle.py_tree_root(pieces, c["fanout"], fold=fold).hex() == want
+        assert (c["root_nonempty"] != c["root_leaf_gated"]) == c["variants_differ"]

@@ -20,4 +20,4 @@ fi
 /opt/rocm/lib/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=thread -fno-omit-frame-pointer \
   -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/tsan/stress.cpp \
   -L"$OUT" -lbsgpu -Wl,-rpath,"$OUT" -o "$OUT/stress"
-TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 ${TSAN_OPTIONS:-}" "$OUT/stress" "$MODE"
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$PWD/tools/tsan/suppressions.txt ${TSAN_OPTIONS:-}" "$OUT/stress" "$MODE"
