@@ -67,6 +67,7 @@ def lib() -> ctypes.CDLL:
         "bsg_params_default": (Params, []),
         "bsg_default_table": (None, [u32p]),
         "bsg_device_count": (ctypes.c_int, []),
+        "bsg_init": (ctypes.c_int, [ctypes.c_int]),
         "bsg_open": (vp, [ctypes.c_int, ctypes.POINTER(Params), u32p, ctypes.POINTER(ctypes.c_int)]),
         "bsg_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
         "bsg_close": (ctypes.c_int, [vp]),
@@ -139,7 +140,10 @@ def lib() -> ctypes.CDLL:
         "bsg_reader_size": (ctypes.c_uint64, [vp]),
         "bsg_reader_free": (None, [vp]),
     }
+    partial = os.environ.get("BSG_LIB_PARTIAL") == "1"  # A/B of older builds (tools/)
     for name, (res, args) in sig.items():
+        if partial and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -169,6 +173,11 @@ def _p(a: np.ndarray, ct):
 
 def device_count() -> int:
     return lib().bsg_device_count()
+
+
+def init(device: int = 0) -> None:
+    """bsg_init: the process's one-time device / kernel / thread start-up, done up front."""
+    _check(lib().bsg_init(device), "bsg_init")
 
 
 def default_table() -> np.ndarray:

@@ -8,6 +8,7 @@
 // host; bsg_engine_finish() is the only synchronisation (and the place where a too-small
 // candidate buffer is grown and the run repeated).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -64,9 +65,19 @@ struct DevBuf {
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Page-locked host memory. Two kinds:
+//  * kernel-visible (default): hipHostMalloc, mapped for the device, so kernels can write
+//    results straight into it (records, counters, snapshots);
+//  * DMA staging (dma_only): an anonymous mapping with transparent huge pages requested, pinned
+//    with hipHostRegister and only ever read by hipMemcpyAsync. On the MI355X box this takes
+//    17 ms per 256 MiB (mostly zero-filling the pages) and 10 ms to free, against 50-65 ms and
+//    29-43 ms for hipHostMalloc / hipHostFree (tools/ubench/pin_cost.cpp,
+//    profiles/r03_pin_cost.log). Falls back to hipHostMalloc if registration fails.
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
+  bool dma_only = false;
+  size_t map_len = 0;  // > 0: p is an mmap of map_len bytes registered with hipHostRegister
   // the device-side address of p (kernels write results straight into pinned host memory)
   void* dev() const {
     void* d = nullptr;
@@ -76,38 +87,110 @@ struct PinBuf {
     }
     return d;
   }
-  hipError_t ensure(size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    if (bytes <= cap) return hipSuccess;
-    if (p) hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
-    if (e != hipSuccess) return e;
-    cap = bytes;
-    return hipSuccess;
+  static constexpr size_t kHuge = 2ull << 20;
+  // allocates into (*q, *len): *len > 0 for the registered mapping, 0 for hipHostMalloc
+  hipError_t alloc(size_t bytes, void** q, size_t* len) const {
+    *q = nullptr;
+    *len = 0;
+    if (dma_only && bytes >= kHuge) {
+      const size_t n = (bytes + kHuge - 1) & ~(kHuge - 1);
+      void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (m != MAP_FAILED) {
+        (void)::madvise(m, n, MADV_HUGEPAGE);
+        if (hipHostRegister(m, n, hipHostRegisterDefault) == hipSuccess) {
+          *q = m;
+          *len = n;
+          return hipSuccess;
+        }
+        (void)hipGetLastError();
+        ::munmap(m, n);
+      }
+    }
+    return hipHostMalloc(q, bytes, hipHostMallocDefault);
   }
+  static void free_(void* q, size_t len) {
+    if (!q) return;
+    if (len) {
+      (void)hipHostUnregister(q);
+      ::munmap(q, len);
+    } else {
+      (void)hipHostFree(q);
+    }
+  }
+  hipError_t ensure(size_t bytes) { return grow(bytes, 0); }
   // ensure() that keeps the first `keep` bytes
   hipError_t grow(size_t bytes, size_t keep) {
+    if (bytes == 0) bytes = 16;
     if (bytes <= cap) return hipSuccess;
     void* q = nullptr;
-    hipError_t e = hipHostMalloc(&q, bytes, hipHostMallocDefault);
+    size_t len = 0;
+    hipError_t e = alloc(bytes, &q, &len);
     if (e != hipSuccess) return e;
     if (keep) std::memcpy(q, p, keep);
-    if (p) hipHostFree(p);
+    free_(p, map_len);
     p = q;
-    cap = bytes;
+    map_len = len;
+    cap = len ? len : bytes;
     return hipSuccess;
   }
   void release() {
-    if (p) hipHostFree(p);
+    free_(p, map_len);
     p = nullptr;
     cap = 0;
+    map_len = 0;
   }
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
 int herr(hipError_t e) { return e == hipSuccess ? BSG_OK : BSG_EDEVICE; }
+
+// HIP streams come from a process-wide pool per device: creating one costs 12-13 ms for each
+// of the process's first four (each gets a hardware queue) and ~4 ms after, destroying one
+// ~3 ms (tools/ubench/first_use.hip, profiles/r03_first_use.log), which a context per file and
+// an engine per tile slot paid every time. Streams go back to the pool instead.
+constexpr size_t kStreamPoolMax = 32;
+std::mutex g_stream_mu;
+std::vector<hipStream_t>& stream_pool(int device) {
+  static auto* pools = new std::vector<std::vector<hipStream_t>>(64);  // never destroyed
+  return (*pools)[(size_t)device & 63];
+}
+hipError_t stream_acquire(int device, hipStream_t* s) {
+  {
+    std::lock_guard<std::mutex> g(g_stream_mu);
+    auto& v = stream_pool(device);
+    if (!v.empty()) {
+      *s = v.back();
+      v.pop_back();
+      return hipSuccess;
+    }
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+// The stream must be idle (callers synchronise it first); the device must be current.
+void stream_release(int device, hipStream_t s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(g_stream_mu);
+    auto& v = stream_pool(device);
+    if (v.size() < kStreamPoolMax) {
+      v.push_back(s);
+      return;
+    }
+  }
+  (void)hipStreamDestroy(s);
+}
+
+// CUs of a device (one attribute query; the device-properties call fills the whole struct and
+// costs milliseconds, which an engine per tile slot paid on every bsg_open)
+int device_cus(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      n <= 0) {
+    (void)hipGetLastError();
+    n = 256;
+  }
+  return n;
+}
 
 // BSG_DEBUG_SYNC=1: synchronise and report after every launch (debugging hangs/faults)
 bool debug_sync() {
@@ -574,9 +657,8 @@ int default_slots() {
 }
 
 struct TileSlot {
-  bsg_engine* eng = nullptr;
+  bsg_engine* eng = nullptr;  // created at the slot's first tile (a small stream needs one)
   DevBuf dbuf;            // carry area + tile + slack
-  PinBuf staging;         // this tile's host bytes
   PinBuf recs;            // records, D2H'd after k_sha
   hipEvent_t h2d_ev = nullptr, done_ev = nullptr;
   // state of the tile currently using the slot
@@ -587,50 +669,83 @@ struct TileSlot {
   uint64_t seg_base = 0, len = 0, nchunks = 0, open_next = 0;
 };
 
+// Host staging of the streaming path: a ring of pinned buffers, independent of the device tiles.
+// The host fills one stage; a full stage is copied (hipMemcpyAsync, on the engine stream of the
+// tile it belongs to) into that tile's device slot right away, so a tile's H2D runs while the
+// host is still filling the rest of it, and the pinned memory a context holds is the ring
+// (4 x 64 MiB: as much host-side slack as one whole tile), not three whole tiles (3 x 256 MiB).
+constexpr int kStages = 4;
+constexpr size_t kStageMax = 64ull << 20;
+struct Stage {
+  PinBuf buf;                // DMA staging (PinBuf::dma_only)
+  hipEvent_t ev = nullptr;   // recorded after the H2D that reads the stage
+  bool inflight = false;     // an H2D from it may still be running
+};
+
 struct bsg_ctx {
   bsg_params params{};
   Params p{};
   int dev = 0;
+  uint32_t table[256];
   size_t tile = 256ull << 20;
   uint64_t carry_cap = kDefaultCarryCap;
   int nslots = default_slots();
   TileSlot slots[kMaxSlots];
-  int cur = 0;              // slot the host is filling
-  size_t fill = 0;
+  Stage stages[kStages];
+  int cur = 0;              // slot of the tile the host is filling
+  size_t fill = 0;          // bytes of the current tile (copied to the device or staged)
+  int scur = 0;             // stage the host is filling
+  size_t sfill = 0;         // bytes in stages[scur] (the current tile's last sfill bytes)
   int prev = -1;            // last submitted slot (its open chunk continues into `cur`)
   std::deque<int> inflight; // submitted slots in stream order
   uint64_t pos = 0;         // stream offset of slots[cur]'s first byte
   uint8_t hist[64];         // the 64 stream bytes before pos
+  uint8_t tail[64];         // the last 64 stream bytes copied to the device so far
   std::deque<bsg_chunk> ready;
   bool closed = false, started = false;
   int sticky = BSG_OK;
 
-  int init(int device, const uint32_t* table) {
+  size_t stage_size() const { return std::min(tile, kStageMax); }
+
+  int init(int device, const uint32_t* tab) {
     dev = device;
-    for (int k = 0; k < nslots; ++k) {
-      TileSlot& t = slots[k];
-      int err = BSG_OK;
-      t.eng = bsg_engine_create(device, table, &err);
-      if (!t.eng) return err;
-      t.eng->snapshot = true;
-      HCHECK(hipEventCreateWithFlags(&t.h2d_ev, hipEventDisableTiming));
-      HCHECK(hipEventCreateWithFlags(&t.done_ev, hipEventDisableTiming));
+    std::memcpy(table, tab ? tab : kBuzhash32Seed1, sizeof table);
+    for (Stage& st : stages) {
+      st.buf.dma_only = true;
+      HCHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
     }
     std::memset(hist, 0, 64);
+    std::memset(tail, 0, 64);
+    return ensure_slot(0);  // the first tile's engine: errors surface at bsg_open
+  }
+
+  int ensure_slot(int i) {
+    TileSlot& t = slots[i];
+    if (t.eng) return BSG_OK;
+    int err = BSG_OK;
+    t.eng = bsg_engine_create(dev, table, &err);
+    if (!t.eng) return err;
+    t.eng->snapshot = true;
+    HCHECK(hipEventCreateWithFlags(&t.h2d_ev, hipEventDisableTiming));
+    HCHECK(hipEventCreateWithFlags(&t.done_ev, hipEventDisableTiming));
     return BSG_OK;
   }
 
   void release() {
-    hipSetDevice(dev);
+    (void)hipSetDevice(dev);
     for (TileSlot& t : slots) {
-      if (t.eng) hipStreamSynchronize(t.eng->stream);
+      if (t.eng) (void)hipStreamSynchronize(t.eng->stream);
       t.dbuf.release();
-      t.staging.release();
       t.recs.release();
-      if (t.h2d_ev) hipEventDestroy(t.h2d_ev);
-      if (t.done_ev) hipEventDestroy(t.done_ev);
+      if (t.h2d_ev) (void)hipEventDestroy(t.h2d_ev);
+      if (t.done_ev) (void)hipEventDestroy(t.done_ev);
       bsg_engine_destroy(t.eng);
       t.eng = nullptr;
+    }
+    for (Stage& st : stages) {
+      st.buf.release();
+      if (st.ev) (void)hipEventDestroy(st.ev);
+      st.ev = nullptr;
     }
   }
 
@@ -730,11 +845,65 @@ struct bsg_ctx {
     return BSG_OK;
   }
 
+  // Copy the staged bytes of the current tile to its device slot (on the slot's engine stream,
+  // behind that slot's previous tile) and move to the next stage.
+  int flush_stage() {
+    if (sfill == 0) return BSG_OK;
+    int rc = ensure_slot(cur);
+    if (rc) return rc;
+    TileSlot& t = slots[cur];
+    HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
+    Stage& st = stages[scur];
+    const uint8_t* src = st.buf.as<uint8_t>();
+    // history for the next tile: the last 64 stream bytes copied so far
+    if (sfill >= 64) {
+      std::memcpy(tail, src + sfill - 64, 64);
+    } else {
+      std::memmove(tail, tail + sfill, 64 - sfill);
+      std::memcpy(tail + 64 - sfill, src, sfill);
+    }
+    HCHECK(hipMemcpyAsync(t.dbuf.as<uint8_t>() + carry_cap + (fill - sfill), st.buf.p, sfill,
+                          hipMemcpyHostToDevice, t.eng->stream));
+    HCHECK(hipEventRecord(st.ev, t.eng->stream));
+    st.inflight = true;
+    scur = (scur + 1) % kStages;
+    sfill = 0;
+    return BSG_OK;
+  }
+
+  // stages[scur] ready to take bytes: its previous H2D has run, and it can hold `need` bytes.
+  // A stream's first stage grows (doubling from 4 MiB) so a small stream pins a few MiB; once
+  // the stream has passed a stage's worth of bytes, stages are allocated whole.
+  static constexpr size_t kMinStaging = 4ull << 20;
+  int stage_ready(size_t need) {
+    Stage& st = stages[scur];
+    if (st.inflight) {
+      HCHECK(hipEventSynchronize(st.ev));
+      st.inflight = false;
+    }
+    const size_t full = stage_size();
+    const bool big = pos + fill >= full;  // past a stage's worth of bytes: whole stages
+    const size_t want = big ? full : std::min(full, std::max(need, kMinStaging));
+    const size_t have = std::min(st.buf.cap, full);
+    if (have >= want) return BSG_OK;
+    const size_t nc = big ? full : std::min(full, std::max(want, 2 * have));
+    HCHECK(st.buf.grow(nc, sfill));
+    return BSG_OK;
+  }
+  size_t stage_room() const {
+    return std::min(stages[scur].buf.cap, stage_size()) - sfill;
+  }
+
   int submit(bool final_seg) {
+    int rc0 = flush_stage();  // every byte of the tile is on its way to the device slot
+    if (rc0) return rc0;
     const int i = cur;
+    if ((rc0 = ensure_slot(i))) return rc0;
     TileSlot& t = slots[i];
     bsg_engine* e = t.eng;
-    int rc0 = reclaim(i);  // the engine and device slot of the tile kSlots back
+    // the engine of the tile kSlots back: its records must be collected before the engine's
+    // buffers are reused (the H2Ds above already queue behind its kernels on the same stream)
+    rc0 = reclaim(i);
     if (rc0) return rc0;
     HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
     uint8_t* base = t.dbuf.as<uint8_t>();
@@ -780,10 +949,6 @@ struct bsg_ctx {
       rc = enqueue_recs(prev);
       if (rc) return rc;
     }
-    if (fill)
-      HCHECK(hipMemcpyAsync(base + carry_cap, t.staging.p, fill, hipMemcpyHostToDevice,
-                            e->stream));
-    HCHECK(hipEventRecord(t.h2d_ev, e->stream));
     e->d_data = base;
     e->descs.assign(1, d);
     e->nstreams = 1;
@@ -797,14 +962,7 @@ struct bsg_ctx {
     t.seg_base = pos;
     t.len = fill;
     inflight.push_back(i);
-    // window history for the next tile = the last 64 stream bytes so far
-    const uint8_t* seg = t.staging.as<uint8_t>();
-    if (fill >= 64) {
-      std::memcpy(hist, seg + fill - 64, 64);
-    } else if (fill) {
-      std::memmove(hist, hist + fill, 64 - fill);
-      std::memcpy(hist + 64 - fill, seg, fill);
-    }
+    std::memcpy(hist, tail, 64);  // window history for the next tile
     pos += fill;
     fill = 0;
     prev = i;
@@ -813,21 +971,8 @@ struct bsg_ctx {
     return BSG_OK;
   }
 
-  // Pinned staging grows with the stream's first tile (doubling from 4 MiB up to the tile), so
-  // a small stream pins a few MiB, not a whole tile: pinning 256 MiB took ~50 ms, most of a
-  // small Write.
-  static constexpr size_t kMinStaging = 4ull << 20;
-  int grow_staging(TileSlot& t, size_t need) {
-    if (need <= t.staging.cap) return BSG_OK;
-    // past its first tile a stream is a big one: later tiles get the whole tile at once
-    const size_t nc = pos > 0 ? tile
-                              : std::min(tile, std::max({need, 2 * t.staging.cap, kMinStaging}));
-    HCHECK(t.staging.grow(nc, fill));
-    return BSG_OK;
-  }
-
-  // Host side of Write: bytes into the current slot's pinned staging (large pieces on several
-  // threads), submitting full tiles as more data arrives.
+  // Host side of Write: bytes into the staging ring (large pieces on several threads), each full
+  // stage on its way to the device at once, full tiles submitted as more data arrives.
   // Stream offsets travel in 40-bit candidate fields (bsgpu_internal.h): 1 TiB per stream.
   static constexpr uint64_t kMaxStream = 1ull << 40;
   bool too_long(size_t n) const { return pos + fill + n >= kMaxStream; }
@@ -839,57 +984,59 @@ struct bsg_ctx {
         int rc = submit(false);
         if (rc) return rc;
       }
-      TileSlot& t = slots[cur];
-      if (fill == 0) {
-        // the staging buffer is free once its last H2D has run; the slot's engine and device
-        // buffer are reclaimed only at submit(), so the host copy overlaps that tile's k_sha
-        HCHECK(hipEventSynchronize(t.h2d_ev));
-      }
-      const size_t k = std::min(n, tile - fill);
-      int rc = grow_staging(t, fill + k);
+      int rc = stage_ready(sfill + std::min(n, tile - fill));
       if (rc) return rc;
-      par_copy(t.staging.as<uint8_t>() + fill, p, k);
+      const size_t k = std::min({n, tile - fill, stage_room()});
+      par_copy(stages[scur].buf.as<uint8_t>() + sfill, p, k);
+      sfill += k;
       fill += k;
       p += k;
       n -= k;
+      // a full stage goes to the device now, except the tile's last one: if the stream ends
+      // here, it is submitted as the final segment
+      if (stage_room() == 0 && fill < tile && (rc = flush_stage())) return rc;
     }
     return poll();
   }
 
   // Zero-copy form of write(): the caller fills pinned staging directly (an io.Reader reads
-  // into it), then commits. The window is the rest of the current tile.
+  // into it), then commits. The window is the rest of the current stage (within the tile).
   int window(uint8_t** p, size_t* cap) {
     if (fill == tile) {
       // The caller may be at EOF, so this tile cannot be the last one submitted as non-final:
-      // hold its last bytes back for the next tile. (A final segment must hold at least one
-      // byte: the flush of the open chunk is emitted by the scan of the final segment's last
-      // strip, and an empty segment has none.)
+      // hold its last bytes (still in the current stage) back for the next tile. (A final
+      // segment must hold at least one byte: the flush of the open chunk is emitted by the scan
+      // of the final segment's last strip, and an empty segment has none.)
       constexpr size_t kHold = 4096;
       uint8_t held[kHold];
-      const size_t hold = std::min(kHold, tile / 2);
-      std::memcpy(held, slots[cur].staging.as<uint8_t>() + tile - hold, hold);
-      fill = tile - hold;
+      const size_t hold = std::min({kHold, tile / 2, sfill});
+      std::memcpy(held, stages[scur].buf.as<uint8_t>() + sfill - hold, hold);
+      sfill -= hold;
+      fill -= hold;
       int rc = submit(false);
       if (rc) return rc;
-      TileSlot& n = slots[cur];
-      HCHECK(hipEventSynchronize(n.h2d_ev));
-      int rc2 = grow_staging(n, hold);  // (fill is 0 here: nothing to keep)
-      if (rc2) return rc2;
-      std::memcpy(n.staging.p, held, hold);
-      fill = hold;
+      if ((rc = stage_ready(hold))) return rc;
+      std::memcpy(stages[scur].buf.p, held, hold);
+      sfill = fill = hold;
     }
-    TileSlot& t = slots[cur];
-    if (fill == 0) HCHECK(hipEventSynchronize(t.h2d_ev));
-    // the window is the staging buffer's free part; a full one grows (keeping what it holds)
-    int rc = grow_staging(t, fill + 1);
+    // the window is the stage's free part (within the tile); a full stage grows or is flushed
+    int rc = stage_ready(sfill + 1);
     if (rc) return rc;
-    *p = t.staging.as<uint8_t>() + fill;
-    *cap = std::min(t.staging.cap, tile) - fill;
+    if (stage_room() == 0) {  // a full stage below the tile's end: move on to the next one
+      if ((rc = flush_stage()) || (rc = stage_ready(1))) return rc;
+    }
+    *p = stages[scur].buf.as<uint8_t>() + sfill;
+    *cap = std::min(stage_room(), tile - fill);
     return BSG_OK;
   }
   int commit(size_t n) {
-    if (n > std::min(slots[cur].staging.cap, tile) - fill || too_long(n)) return BSG_EINVAL;
+    if (n > std::min(stage_room(), tile - fill) || too_long(n)) return BSG_EINVAL;
+    sfill += n;
     fill += n;
+    if (stage_room() == 0 && fill < tile) {
+      int rc = flush_stage();
+      if (rc) return rc;
+    }
     return poll();
   }
 
@@ -914,18 +1061,24 @@ struct bsg_ctx {
     for (int k = 0; k < nslots; ++k) {
       TileSlot& t = slots[k];
       if (t.eng) HCHECK(hipStreamSynchronize(t.eng->stream));
-      if (t.h2d_ev) HCHECK(hipEventSynchronize(t.h2d_ev));
       t.busy = false;
       t.sel_read = t.recs_enq = false;
       if (t.eng) t.eng->enqueued = false;
+    }
+    for (Stage& st : stages) {
+      if (st.inflight) HCHECK(hipEventSynchronize(st.ev));
+      st.inflight = false;
     }
     inflight.clear();
     ready.clear();
     cur = 0;
     fill = 0;
+    scur = 0;
+    sfill = 0;
     prev = -1;
     pos = 0;
     std::memset(hist, 0, 64);
+    std::memset(tail, 0, 64);
     closed = false;
     started = false;
     sticky = BSG_OK;
@@ -980,6 +1133,37 @@ bsg_params bsg_params_default(void) {
 
 void bsg_default_table(uint32_t out[256]) { std::memcpy(out, kBuzhash32Seed1, 1024); }
 
+int bsg_init(int device) {
+  if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
+  HCHECK(hipSetDevice(device));
+  // streams for the pool: one per hardware queue the process gets (GPU_MAX_HW_QUEUES, 4), the
+  // ones a streaming context, a hasher and a batch engine take first
+  constexpr int kWarmStreams = 4;
+  hipStream_t s[kWarmStreams] = {};
+  int got = 0;
+  hipError_t e = hipSuccess;
+  for (; got < kWarmStreams && e == hipSuccess; ++got) e = stream_acquire(device, &s[got]);
+  if (e != hipSuccess) --got;
+  // the device context, the copy engines and libbsgpu's code object: one small H2D, kernel and
+  // D2H on each warm stream (the process's first DMA copy alone costs tens of ms)
+  void* d = nullptr;
+  PinBuf h;
+  if (e == hipSuccess) e = hipMalloc(&d, 4096);
+  if (e == hipSuccess) e = h.ensure(4096);
+  for (int i = 0; i < got && e == hipSuccess; ++i) {
+    e = hipMemcpyAsync(d, h.p, 2048, hipMemcpyHostToDevice, s[i]);
+    if (e == hipSuccess) e = launch_copy_out(d, static_cast<uint8_t*>(d) + 2048, 64, s[i]);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.p, d, 64, hipMemcpyDeviceToHost, s[i]);
+    if (e == hipSuccess) e = hipStreamSynchronize(s[i]);
+  }
+  if (d) (void)hipFree(d);
+  h.release();
+  for (int i = 0; i < got; ++i) stream_release(device, s[i]);
+  HCHECK(e);
+  bsg::parallel_for(bsg::copy_threads(), [](size_t) {});  // the host copy pool's threads
+  return BSG_OK;
+}
+
 int bsg_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -1004,14 +1188,12 @@ bsg_engine* bsg_engine_create(int device, const uint32_t* table, int* err) {
   }
   e->dev = device;
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+      stream_acquire(device, &e->stream) != hipSuccess) {
     delete e;
     *err = BSG_EDEVICE;
     return nullptr;
   }
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-    e->num_cus = prop.multiProcessorCount;
+  e->num_cus = device_cus(device);
   if (e->table.ensure(1024) != hipSuccess ||
       hipMemcpy(e->table.p, table ? table : kBuzhash32Seed1, 1024, hipMemcpyHostToDevice) !=
           hipSuccess) {
@@ -1040,7 +1222,7 @@ void bsg_engine_destroy(bsg_engine* e) {
   e->h_ctr.release();
   e->h_snap.release();
   if (e->sel_ev) hipEventDestroy(e->sel_ev);
-  if (e->stream) hipStreamDestroy(e->stream);
+  if (e->stream) stream_release(e->dev, e->stream);
   delete e;
 }
 
@@ -1433,9 +1615,7 @@ int bsg_fill_splitmix(int device, uint8_t* d_ptr, uint64_t nbytes, uint64_t seed
   if (!d_ptr && nbytes) return BSG_EINVAL;
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
   HCHECK(hipSetDevice(device));
-  hipDeviceProp_t prop;
-  int cus = 256;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess) cus = prop.multiProcessorCount;
+  const int cus = device_cus(device);
   if (nbytes) HCHECK(launch_fill_splitmix(d_ptr, nbytes, seed, (hipStream_t)stream, cus));
   return BSG_OK;
 }
@@ -1574,10 +1754,8 @@ bsg_hasher* bsg_hasher_new(int device) {
   bsg_hasher* h = new (std::nothrow) bsg_hasher();
   if (!h) return nullptr;
   h->dev = device;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-    h->num_cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  h->num_cus = device_cus(device);
+  if (stream_acquire(device, &h->stream) != hipSuccess) {
     delete h;
     return nullptr;
   }
@@ -1628,7 +1806,7 @@ void bsg_hasher_free(bsg_hasher* h) {
   h->stage.release();
   h->dstage.release();
   if (h->eng) bsg_engine_destroy(h->eng);
-  if (h->stream) hipStreamDestroy(h->stream);
+  if (h->stream) stream_release(h->dev, h->stream);
   delete h;
 }
 

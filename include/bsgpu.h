@@ -72,6 +72,10 @@ bsg_params bsg_params_default(void);
 /* The buzhash32 table used when callers pass table == NULL: rollinghash's GenerateHashes(1). */
 void bsg_default_table(uint32_t out[256]);
 int bsg_device_count(void);
+/* Optional, once per process: makes `device` current, creates its HIP context, loads libbsgpu's
+ * kernels and starts the host copy threads — the one-time cost (tens of ms) that the first call
+ * of any other entry point pays otherwise. A server calls it at start-up. */
+int bsg_init(int device);
 
 /* ---- streaming split.Writer (bytes arrive from host memory) ---- */
 typedef struct bsg_ctx bsg_ctx;
@@ -81,8 +85,8 @@ bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table /*
  * and hashed on the device as they fill. A stream may hold up to 2^40 - 1 bytes (1 TiB; stream
  * offsets travel in 40-bit fields on the device): a Write past that returns BSG_EINVAL. */
 int bsg_write(bsg_ctx* ctx, const uint8_t* p, size_t n);
-/* Zero-copy Write: *p / *cap = the free rest of the current pinned staging buffer (never more
- * than the rest of the tile; the buffer grows from 4 MiB to the tile size as the stream does,
+/* Zero-copy Write: *p / *cap = the free rest of the current pinned staging buffer (at most
+ * 64 MiB and never more than the rest of the tile; a stream's first buffer grows from 4 MiB,
  * so early windows are smaller); the caller fills up to *cap bytes there (e.g. an io.Reader
  * reads straight into it) and commits n of them. Same stream semantics as bsg_write; the
  * window is valid until the next call on ctx. */
@@ -93,9 +97,11 @@ int bsg_close(bsg_ctx* ctx);
 /* Number of finished chunks not yet drained, and drain up to cap of them (stream order). */
 size_t bsg_pending(const bsg_ctx* ctx);
 size_t bsg_drain(bsg_ctx* ctx, bsg_chunk* out, size_t cap);
-/* Staging tile size in bytes (default 256 MiB); call before the first write. Three tiles are
+/* Device tile size in bytes (default 256 MiB); call before the first write. Three tiles are
  * in flight at once (BSG_STREAM_SLOTS overrides): tile i+1's split starts as soon as tile i's
- * boundaries are known, while tile i's SHA-256 is still running. */
+ * boundaries are known, while tile i's SHA-256 is still running. Host bytes pass through a
+ * ring of four pinned staging buffers of min(tile, 64 MiB), each copied to its tile's device
+ * slot as soon as it is full. */
 int bsg_set_tile(bsg_ctx* ctx, size_t tile_bytes);
 /* Longest open chunk carried between tiles as bytes on the device (default 8 MiB); a longer
  * one is carried as a SHA-256 midstate, which makes the next tile wait for this tile's hashes.

@@ -13,10 +13,10 @@ which the last chain would end under several schedules, from measured stage cost
   position-major         all streams scanned front to back together; a chunk's chain starts
                          once the scan front has passed its end (its length is known)
 
-Only the chain bound is modelled: it ignores that per-lane SHA-256 work (which keeps the chip
-busy until the chain ends today) would have to shrink as well.
+The chain bound of each schedule is printed, then the work bound: the scan and the per-lane
+SHA-256 blocks share the chip, at the per-lane throughput measured by tools/ubench/lanes_occ.hip.
 
-  python tools/sim_early_chain.py [--scan-ms 3.76] [--sel-ms 0.27] [--us-per-block 1.157]
+  python tools/sim_early_chain.py [--scan-ms 3.73] [--sel-ms 0.27] [--us-per-block 1.16]
 """
 from __future__ import annotations
 
@@ -69,6 +69,12 @@ def main() -> None:
     ap.add_argument("--sel-ms", type=float, default=0.27, help="selection kernels")
     ap.add_argument("--us-per-block", type=float, default=1.157, help="solo-chain block time")
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--lane-rate1", type=float, default=23.8, help="k blocks/us, 1 wave/SIMD")
+    ap.add_argument("--lane-rate3", type=float, default=27.8, help="k blocks/us, 3 waves/SIMD")
+    ap.add_argument("--wave-min-blocks", type=int, default=4065,
+                    help="jobs this long go to wave tickets (bench sha_path.long_thresh)")
+    ap.add_argument("--tickets", type=int, default=240, help="wave tickets (sha_path)")
+    ap.add_argument("--simds", type=int, default=1024)
     args = ap.parse_args()
 
     a = chunk_table(args.streams, args.stream_mib, args.threads)
@@ -94,6 +100,30 @@ def main() -> None:
         print(f"  {P:3d} position phases                      {end.max():.3f}")
     fr = (o + ln) / L * args.scan_ms + args.sel_ms + nb * blk
     print(f"  position-major, chain at its chunk's end {fr.max():.3f}")
+    # a chain needs its chunk's START, not its end. With a position-major
+    # scan the front passes a chunk in len / (L / scan_ms), so starting at the start can gain
+    # at most that (a 766 KB chunk: 0.04 ms).
+    fs = o / L * args.scan_ms + args.sel_ms + nb * blk
+    print(f"  position-major, chain at its chunk's start {fs.max():.3f}")
+
+    # The work bound: the chip must also do the scan and every per-lane SHA-256 block, and the
+    # two share it (both VALU-bound). Per-lane throughput from tools/ubench/lanes_occ.hip
+    # (profiles/r03_lanes_occ.log): 23.8 k blocks/us chip-wide at one wave per SIMD (k_sha's
+    # occupancy), 27.8 k at three; a SIMD running a wave-mode chain does ~1/28 of a per-lane
+    # SIMD's blocks, so the tickets' SIMDs are (nearly) lost to the per-lane work while they run.
+    blocks = int(nb.sum())
+    lane_blocks = blocks - int(nb[nb >= args.wave_min_blocks].sum())
+    print(f"work bound: {blocks / 1e6:.1f} M blocks in all, {lane_blocks / 1e6:.1f} M per-lane "
+          f"(jobs under {args.wave_min_blocks} blocks)")
+    for occ, rate in (("1 wave/SIMD", args.lane_rate1), ("3 waves/SIMD", args.lane_rate3)):
+        lane_ms = lane_blocks / (rate * 1e6)
+        busy = args.tickets / args.simds  # share of the chip the wave tickets hold
+        t_sha = lane_ms / (1 - busy)
+        print(f"  {occ:13s}: per-lane work {lane_ms:.2f} ms of full chip, {t_sha:.2f} ms with "
+              f"{args.tickets} SIMDs on wave tickets; scan + selection + SHA-256 = "
+              f"{args.scan_ms + args.sel_ms + t_sha:.2f} ms")
+    print("  a step can end no earlier than the larger of the chain bound of its schedule and "
+          "the work bound")
 
 
 if __name__ == "__main__":
