@@ -1160,8 +1160,43 @@ int bsg_init(int device) {
   h.release();
   for (int i = 0; i < got; ++i) stream_release(device, s[i]);
   HCHECK(e);
+  // every kernel of the split and hash paths once (HIP loads a kernel at its first launch,
+  // ~0.5 ms each, ~20 of them): a 64 KiB split, the same bytes as one blob, one blob per lane
+  int rc = BSG_OK;
+  bsg_engine* eng = bsg_engine_create(device, nullptr, &rc);
+  if (!eng) return rc;
+  constexpr uint64_t kWarm = 64 << 10;
+  uint8_t* buf = static_cast<uint8_t*>(bsg_device_malloc(device, kWarm + kReadSlack));
+  const uint64_t off = 0, len = kWarm;
+  uint64_t n = 0;
+  if (!buf) rc = BSG_ENOMEM;
+  if (rc == BSG_OK) rc = bsg_fill_splitmix(device, buf, kWarm, 1, eng->stream);
+  if (rc == BSG_OK) rc = bsg_engine_run(eng, buf, &off, &len, 1, nullptr);
+  if (rc == BSG_OK) rc = bsg_engine_finish(eng, &n);
+  if (rc == BSG_OK) rc = bsg_engine_hash(eng, buf, &off, &len, 1);
+  if (rc == BSG_OK) rc = bsg_engine_finish(eng, &n);
+  if (rc == BSG_OK) {
+    uint8_t ref[32];
+    uint8_t blob[64] = {0};
+    const uint64_t boff = 0, blen = sizeof blob;
+    bsg_hasher* hs = bsg_hasher_new(device);
+    rc = hs ? bsg_hasher_sum(hs, blob, &boff, &blen, 1, ref) : BSG_EDEVICE;
+    bsg_hasher_free(hs);
+  }
+  bsg_device_free(device, buf);
+  bsg_engine_destroy(eng);
+  if (rc) return rc;
   bsg::parallel_for(bsg::copy_threads(), [](size_t) {});  // the host copy pool's threads
-  return BSG_OK;
+  // the streaming path once (registered staging, H2D from it, kernels writing into mapped
+  // host memory, events): first uses the process would otherwise pay in its first Writer
+  bsg_ctx* c = bsg_open(device, nullptr, nullptr, &rc);
+  if (!c) return rc;
+  std::vector<uint8_t> bytes(kWarm);
+  for (size_t i = 0; i < bytes.size(); ++i) bytes[i] = (uint8_t)(i * 2654435761u >> 24);
+  rc = bsg_write(c, bytes.data(), bytes.size());
+  if (rc == BSG_OK) rc = bsg_close(c);
+  bsg_free(c);
+  return rc;
 }
 
 int bsg_device_count(void) {

@@ -72,9 +72,11 @@ bsg_params bsg_params_default(void);
 /* The buzhash32 table used when callers pass table == NULL: rollinghash's GenerateHashes(1). */
 void bsg_default_table(uint32_t out[256]);
 int bsg_device_count(void);
-/* Optional, once per process: makes `device` current, creates its HIP context, loads libbsgpu's
- * kernels and starts the host copy threads — the one-time cost (tens of ms) that the first call
- * of any other entry point pays otherwise. A server calls it at start-up. */
+/* Optional, once per process: makes `device` current, creates its HIP context and a few HIP
+ * streams (kept in the library's stream pool), initialises the copy engines, loads every kernel
+ * of the split and hash paths (one tiny split and hash) and starts the host copy threads — the
+ * one-time cost (~50 ms) that the first Writer of a process pays otherwise. A server calls it
+ * at start-up. */
 int bsg_init(int device);
 
 /* ---- streaming split.Writer (bytes arrive from host memory) ---- */
