@@ -78,6 +78,9 @@ def lib() -> ctypes.CDLL:
         "bsg_write_window": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_void_p),
                                             ctypes.POINTER(ctypes.c_size_t)]),
         "bsg_write_commit": (ctypes.c_int, [vp, ctypes.c_size_t]),
+        "bsg_host_register": (ctypes.c_int, [vp, ctypes.c_size_t]),
+        "bsg_host_unregister": (ctypes.c_int, [vp]),
+        "bsg_write_pinned": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
         "bsg_free": (None, [vp]),
         "bsg_reset": (ctypes.c_int, [vp]),
         "bsg_engine_create": (vp, [ctypes.c_int, u32p, ctypes.POINTER(ctypes.c_int)]),
@@ -268,6 +271,15 @@ class Hasher:
             pass
 
 
+def host_register(ptr: int, n: int) -> None:
+    """bsg_host_register: page-lock caller memory for bsg_write_pinned."""
+    _check(lib().bsg_host_register(ptr, n), "bsg_host_register")
+
+
+def host_unregister(ptr: int) -> None:
+    _check(lib().bsg_host_unregister(ptr), "bsg_host_unregister")
+
+
 def fill_splitmix(ptr: int, nbytes: int, seed: int, stream: int | None = None,
                   device: int = 0) -> None:
     _check(lib().bsg_fill_splitmix(device, ptr, nbytes, seed, stream), "bsg_fill_splitmix")
@@ -425,6 +437,11 @@ class StreamingSplitter:
         a = _as_u8(data)
         _check(lib().bsg_write(self.h, a.ctypes.data, a.nbytes), "bsg_write")
         return a.nbytes
+
+    def write_pinned(self, ptr: int, n: int) -> None:
+        """bsg_write_pinned: n bytes at ptr, host memory registered with host_register; the
+        caller keeps them unchanged until close()."""
+        _check(lib().bsg_write_pinned(self.h, ptr, n), "bsg_write_pinned")
 
     def close(self) -> None:
         _check(lib().bsg_close(self.h), "bsg_close")

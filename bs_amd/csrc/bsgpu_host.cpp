@@ -854,14 +854,7 @@ struct bsg_ctx {
     TileSlot& t = slots[cur];
     HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
     Stage& st = stages[scur];
-    const uint8_t* src = st.buf.as<uint8_t>();
-    // history for the next tile: the last 64 stream bytes copied so far
-    if (sfill >= 64) {
-      std::memcpy(tail, src + sfill - 64, 64);
-    } else {
-      std::memmove(tail, tail + sfill, 64 - sfill);
-      std::memcpy(tail + 64 - sfill, src, sfill);
-    }
+    tail_append(st.buf.as<uint8_t>(), sfill);  // history for the next tile
     HCHECK(hipMemcpyAsync(t.dbuf.as<uint8_t>() + carry_cap + (fill - sfill), st.buf.p, sfill,
                           hipMemcpyHostToDevice, t.eng->stream));
     HCHECK(hipEventRecord(st.ev, t.eng->stream));
@@ -995,6 +988,54 @@ struct bsg_ctx {
       // a full stage goes to the device now, except the tile's last one: if the stream ends
       // here, it is submitted as the final segment
       if (stage_room() == 0 && fill < tile && (rc = flush_stage())) return rc;
+    }
+    return poll();
+  }
+
+  // Appends bytes that already went to the device (or are on their way) to the running tail.
+  void tail_append(const uint8_t* q, size_t k) {
+    if (k >= 64) {
+      std::memcpy(tail, q + k - 64, 64);
+    } else {
+      std::memmove(tail, tail + k, 64 - k);
+      std::memcpy(tail + 64 - k, q, k);
+    }
+  }
+
+  // write() from host memory the caller registered (bsg_host_register): no staging copy, the
+  // H2D reads the caller's bytes directly, on the engine stream of the tile they belong to. The
+  // last bytes (up to 4 KiB) of a segment that completes a tile are staged instead, so that a
+  // full tile always keeps unflushed bytes that window() can hold back for the next tile (a
+  // final segment needs at least one byte).
+  int write_pinned(const uint8_t* q, size_t n) {
+    if (too_long(n)) return BSG_EINVAL;
+    while (n) {
+      if (fill == tile) {
+        int rc = submit(false);
+        if (rc) return rc;
+      }
+      int rc = flush_stage();  // staged bytes of this tile go first (offsets stay in order)
+      if (rc) return rc;
+      if ((rc = ensure_slot(cur))) return rc;
+      TileSlot& t = slots[cur];
+      HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
+      const size_t k = std::min(n, tile - fill);
+      const size_t staged = fill + k == tile ? std::min<size_t>(k, 4096) : 0;
+      const size_t direct = k - staged;
+      if (direct) {
+        HCHECK(hipMemcpyAsync(t.dbuf.as<uint8_t>() + carry_cap + fill, q, direct,
+                              hipMemcpyHostToDevice, t.eng->stream));
+        tail_append(q, direct);
+        fill += direct;
+      }
+      if (staged) {
+        if ((rc = stage_ready(staged))) return rc;
+        std::memcpy(stages[scur].buf.as<uint8_t>(), q + direct, staged);
+        sfill = staged;
+        fill += staged;
+      }
+      q += k;
+      n -= k;
     }
     return poll();
   }
@@ -1457,6 +1498,30 @@ int bsg_write(bsg_ctx* c, const uint8_t* p, size_t n) {
   if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
   c->started = true;
   int rc = c->write(p, n);
+  if (rc) c->sticky = rc;
+  return rc;
+}
+
+int bsg_host_register(void* p, size_t n) {
+  if (!p || !n) return BSG_EINVAL;
+  HCHECK(hipHostRegister(p, n, hipHostRegisterDefault));
+  return BSG_OK;
+}
+
+int bsg_host_unregister(void* p) {
+  if (!p) return BSG_EINVAL;
+  HCHECK(hipHostUnregister(p));
+  return BSG_OK;
+}
+
+int bsg_write_pinned(bsg_ctx* c, const uint8_t* p, size_t n) {
+  if (!c) return BSG_EINVAL;
+  if (c->closed) return BSG_ESTATE;
+  if (c->sticky) return c->sticky;
+  if (n && !p) return BSG_EINVAL;
+  if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
+  c->started = true;
+  int rc = c->write_pinned(p, n);
   if (rc) c->sticky = rc;
   return rc;
 }

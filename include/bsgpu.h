@@ -94,6 +94,15 @@ int bsg_write(bsg_ctx* ctx, const uint8_t* p, size_t n);
  * window is valid until the next call on ctx. */
 int bsg_write_window(bsg_ctx* ctx, uint8_t** p, size_t* cap);
 int bsg_write_commit(bsg_ctx* ctx, size_t n);
+/* Page-locks host memory the caller owns (hipHostRegister) so that bsg_write_pinned can copy
+ * from it to the device without a staging copy; bsg_host_unregister undoes it. */
+int bsg_host_register(void* p, size_t n);
+int bsg_host_unregister(void* p);
+/* bsg_write from memory registered with bsg_host_register: the H2D reads p[0..n) directly and
+ * asynchronously, so the caller keeps those bytes unchanged and registered until the chunks
+ * covering them have been drained (at the latest, until bsg_close / bsg_reset returns). Same
+ * stream semantics as bsg_write. */
+int bsg_write_pinned(bsg_ctx* ctx, const uint8_t* p, size_t n);
 /* Flushes the final chunk (hashsplit Splitter.Close). Idempotent. */
 int bsg_close(bsg_ctx* ctx);
 /* Number of finished chunks not yet drained, and drain up to cap of them (stream order). */

@@ -242,3 +242,30 @@ def test_writer_root_on_tree_fold_fixture(gpu):
         _, root = write_all(gpu, memoryview(data), piece=32 * 1024, bits=c["bits"],
                             min_size=c["min_size"], fanout=c["fanout"])
         assert root.hex() == c["root_nonempty"], c["name"]
+
+
+@pytest.mark.parametrize("tile,sizes", [
+    (8 << 20, [8 << 20, 100]),                    # a pinned Write fills the tile, then a small one
+    (8 << 20, [8 << 20]),                         # ... and the stream ends on the tile boundary
+    (8 << 20, [4 << 20, 4 << 20, 3, 5 << 20]),    # two pinned Writes complete a tile
+    ((5 << 20) + 3, [6 << 20, 1, (4 << 20) + 7, 10 << 20, 65536]),
+    (8 << 20, [1000, 9 << 20, 333, 7 << 20 + 5]),  # small (staged) and large (pinned) mixed
+])
+def test_writer_pinned_and_staged_writes(gpu, oracle, table, tile, sizes):
+    """Writes of 4 MiB and more go to the device straight from their registered piece
+    (bsg_write_pinned), smaller ones through the staging ring; any mix, any tile boundary."""
+    from bs_amd.synth import splitmix_array
+    data = splitmix_array(0x51CE, sum(sizes))
+    st = gpu.MemStore()
+    w = gpu.Writer(st, tile=tile, bits=14, min_size=256)
+    mv = memoryview(data)
+    o = 0
+    for n in sizes:
+        w.write(mv[o:o + n])
+        o += n
+    w.close()
+    want, _ = oracle.writer_root(table, data, bits=14, min_size=256)
+    assert w.root == want
+    assert gpu.Reader(st, w.root).read_all() == data.tobytes()
+    w.free()
+    st.free()

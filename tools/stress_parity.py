@@ -1,5 +1,7 @@
-"""Long randomized parity run (not part of pytest): many seeded draws of batch and streaming
-splits against the oracle. python tools/stress_parity.py [N] -- prints a line per 20 draws."""
+"""Long randomized parity run (not part of pytest): many seeded draws of batch splits, streaming
+splits and (round 3) C++ split.Writer runs with staged and pinned Writes mixed, against the
+oracle. python tools/stress_parity.py [N] [seed_base] -- prints a line per 20 draws.
+STRESS_WRITER=0 restores the round-1/2 mix (batch and streaming draws only)."""
 import os
 import sys
 import time
@@ -28,7 +30,26 @@ def main():
         if rng.random() < 0.1:   # the full ranges split.Bits / split.MinSize accept
             bits = int(rng.choice([4, 6, 8, 12, 33, 40]))
             mn = int(rng.choice([1, 17, 63, 64]))
-        if d % 2 == 0:  # batch of streams, lengths up to 8 MB
+        kind = d % 3 if os.environ.get("STRESS_WRITER", "1") == "1" else d % 2
+        if kind == 2:  # the C++ split.Writer: staged (< 4 MiB) and pinned (>= 4 MiB) Writes mixed
+            n = int(rng.integers(0, 40_000_000))
+            data = splitmix_array(3_000_000 + d, n)
+            tile = int(rng.choice([65536, 1 << 20, 5 << 20, 16 << 20, 256 << 20]))
+            fo = int(rng.choice([2, 4, 8]))
+            st = bsgpu.MemStore()
+            w = bsgpu.Writer(st, bits=bits, min_size=mn, fanout=fo, tile=tile)
+            mv = memoryview(data)
+            pos = 0
+            while pos < n:
+                k = int(rng.choice([1000, 65536, 1 << 20, 4 << 20, 9 << 20]))
+                w.write(mv[pos:pos + k])
+                pos += k
+            w.close()
+            want, _ = O.writer_root(table, data, bits=bits, min_size=mn, fanout=fo)
+            assert w.root == want, ("writer", d, bits, mn, fo, n, tile)
+            w.free()
+            st.free()
+        elif kind == 0:  # batch of streams, lengths up to 8 MB
             ns = int(rng.integers(1, 40))
             lens = [int(x) for x in rng.integers(0, 8_000_000, size=ns)]
             arrs = [splitmix_array(1_000_000 + 97 * d + i, n) for i, n in enumerate(lens)]
