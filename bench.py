@@ -213,9 +213,10 @@ def chain_roofline(diag: dict) -> dict | None:
 
 
 def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
-    """The streaming path from host memory: bsg_write of 32 MiB pieces (copy into pinned
-    staging, hipMemcpyAsync H2D per 256 MiB tile, three tiles in flight) -> split + SHA-256 ->
-    records D2H -> bsg_drain. Best of 3 after one warm-up on the same context (bsg_reset)."""
+    """The streaming path from host memory: bsg_write of 32 MiB pieces (copy into a ring of
+    pinned stages, each copied H2D into its 256 MiB device tile as it fills, three tiles in
+    flight) -> split + SHA-256 -> records D2H -> bsg_drain. Best of 3 after one warm-up on the
+    same context (bsg_reset)."""
     if mib <= 0:
         return None
     from bs_amd import bsgpu
@@ -240,8 +241,9 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
             best = dt
     w.free()
     return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "chunks": nch,
-            "path": "host memory -> bsg_write (pinned staging, H2D) -> split + SHA-256 -> "
-                    "records in host memory; tile 256 MiB, 3 tiles in flight"}
+            "path": "host memory -> bsg_write (ring of 4 x 64 MiB pinned stages, each copied "
+                    "H2D as it fills) -> split + SHA-256 -> records in host memory; tile 256 MiB, "
+                    "3 tiles in flight"}
 
 
 # rocprofv3 names of each stage's kernels (k_sha: two instantiations launched back to back, one of
