@@ -73,6 +73,27 @@ struct DevBuf {
 //    17 ms per 256 MiB (mostly zero-filling the pages) and 10 ms to free, against 50-65 ms and
 //    29-43 ms for hipHostMalloc / hipHostFree (tools/ubench/pin_cost.cpp,
 //    profiles/r03_pin_cost.log). Falls back to hipHostMalloc if registration fails.
+// Host ThreadSanitizer builds (tools/tsan_host.sh): hipHostMalloc / hipHostFree recycle pinned
+// buffers between threads under the HIP runtime's own (uninstrumented) locks, which TSan cannot
+// see; a release before every free and an acquire after every allocation restore the
+// happens-before a real allocator lock gives, so reuse of a freed buffer by another context is
+// not reported as a race.
+#if defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+#define BSG_TSAN 1
+#endif
+#endif
+#ifdef BSG_TSAN
+extern "C" void __tsan_acquire(void* addr);
+extern "C" void __tsan_release(void* addr);
+static char g_tsan_pinned_sync;
+static inline void tsan_after_alloc() { __tsan_acquire(&g_tsan_pinned_sync); }
+static inline void tsan_before_free() { __tsan_release(&g_tsan_pinned_sync); }
+#else
+static inline void tsan_after_alloc() {}
+static inline void tsan_before_free() {}
+#endif
+
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -106,7 +127,9 @@ struct PinBuf {
         ::munmap(m, n);
       }
     }
-    return hipHostMalloc(q, bytes, hipHostMallocDefault);
+    const hipError_t e = hipHostMalloc(q, bytes, hipHostMallocDefault);
+    tsan_after_alloc();
+    return e;
   }
   static void free_(void* q, size_t len) {
     if (!q) return;
@@ -114,6 +137,7 @@ struct PinBuf {
       (void)hipHostUnregister(q);
       ::munmap(q, len);
     } else {
+      tsan_before_free();
       (void)hipHostFree(q);
     }
   }

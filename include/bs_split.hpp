@@ -283,12 +283,9 @@ class Writer {
   struct Piece {
     std::shared_ptr<uint8_t> buf;
     size_t size = 0;
-    size_t map_len = 0;       // > 0: buf is its own mapping of this many bytes
-    bool registered = false;  // page-locked for direct H2D (bsg_host_register)
   };
   std::deque<Piece> pieces_;
   Status Copy(const uint8_t* p, size_t n, uint8_t* dst);  // into dst and pinned staging
-  void Unregister(Piece& piece);
   uint64_t base_ = 0;          // stream offset of pieces_.front()[0]
   uint64_t end_ = 0;           // stream offset one past the last byte written
   uint64_t emitted_ = 0;       // stream offset of the next chunk to emit

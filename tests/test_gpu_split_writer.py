@@ -245,15 +245,15 @@ def test_writer_root_on_tree_fold_fixture(gpu):
 
 
 @pytest.mark.parametrize("tile,sizes", [
-    (8 << 20, [8 << 20, 100]),                    # a pinned Write fills the tile, then a small one
+    (8 << 20, [8 << 20, 100]),                    # a Write fills the tile, then a small one
     (8 << 20, [8 << 20]),                         # ... and the stream ends on the tile boundary
-    (8 << 20, [4 << 20, 4 << 20, 3, 5 << 20]),    # two pinned Writes complete a tile
+    (8 << 20, [4 << 20, 4 << 20, 3, 5 << 20]),    # two Writes complete a tile
     ((5 << 20) + 3, [6 << 20, 1, (4 << 20) + 7, 10 << 20, 65536]),
-    (8 << 20, [1000, 9 << 20, 333, 7 << 20 + 5]),  # small (staged) and large (pinned) mixed
+    (8 << 20, [1000, 9 << 20, 333, 7 << 20 + 5]),  # small and large mixed
 ])
-def test_writer_pinned_and_staged_writes(gpu, oracle, table, tile, sizes):
-    """Writes of 4 MiB and more go to the device straight from their registered piece
-    (bsg_write_pinned), smaller ones through the staging ring; any mix, any tile boundary."""
+def test_writer_large_and_small_writes(gpu, oracle, table, tile, sizes):
+    """Large and small Writes mixed, across stage and tile boundaries of the staging ring (a
+    Write that fills a tile exactly, followed by a small one or by Close)."""
     from bs_amd.synth import splitmix_array
     data = splitmix_array(0x51CE, sum(sizes))
     st = gpu.MemStore()

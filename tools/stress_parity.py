@@ -1,5 +1,5 @@
 """Long randomized parity run (not part of pytest): many seeded draws of batch splits, streaming
-splits and (round 3) C++ split.Writer runs with staged and pinned Writes mixed, against the
+splits and (round 3) C++ split.Writer runs with small and large Writes mixed, against the
 oracle. python tools/stress_parity.py [N] [seed_base] -- prints a line per 20 draws.
 STRESS_WRITER=0 restores the round-1/2 mix (batch and streaming draws only)."""
 import os
@@ -31,7 +31,7 @@ def main():
             bits = int(rng.choice([4, 6, 8, 12, 33, 40]))
             mn = int(rng.choice([1, 17, 63, 64]))
         kind = d % 3 if os.environ.get("STRESS_WRITER", "1") == "1" else d % 2
-        if kind == 2:  # the C++ split.Writer: staged (< 4 MiB) and pinned (>= 4 MiB) Writes mixed
+        if kind == 2:  # the C++ split.Writer: Writes of 1 KB to 9 MiB mixed, tiles 64 KiB-256 MiB
             n = int(rng.integers(0, 40_000_000))
             data = splitmix_array(3_000_000 + d, n)
             tile = int(rng.choice([65536, 1 << 20, 5 << 20, 16 << 20, 256 << 20]))
