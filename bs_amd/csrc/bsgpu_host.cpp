@@ -700,6 +700,60 @@ struct TileSlot {
 // (4 x 64 MiB: as much host-side slack as one whole tile), not three whole tiles (3 x 256 MiB).
 constexpr int kStages = 4;
 constexpr size_t kStageMax = 64ull << 20;
+// Full-size stages (kStageMax) are shared process-wide: a context takes them from this pool as
+// its stream grows past a stage and gives them back at bsg_reset / bsg_free, so an idle pooled
+// context holds no pinned staging, N concurrent contexts share what they use, and bsg_init can
+// pin a ring's worth ahead of the first Writer. (Smaller stages — small tiles, a stream's first
+// stage while it grows — stay with their context.)
+class StagePool {
+ public:
+  static StagePool& get() {
+    static auto* p = new StagePool();  // never destroyed (its buffers live until exit)
+    return *p;
+  }
+  bool take(PinBuf* out) {  // out: empty
+    std::lock_guard<std::mutex> g(mu_);
+    if (free_.empty()) return false;
+    *out = free_.back();
+    free_.pop_back();
+    return true;
+  }
+  void give(PinBuf* b) {  // takes b's buffer if it is a full-size one; b is empty afterwards
+    if (!b->p) return;
+    if (b->cap >= kStageMax && b->map_len) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (free_.size() < kMaxFree) {
+        free_.push_back(*b);
+        *b = PinBuf{};
+        b->dma_only = true;
+        return;
+      }
+    }
+    b->release();
+  }
+  int fill(int n) {  // bsg_init: make sure n full-size stages are pinned and waiting
+    for (;;) {
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if ((int)free_.size() >= n) return BSG_OK;
+      }
+      PinBuf b;
+      b.dma_only = true;
+      if (b.ensure(kStageMax) != hipSuccess) return BSG_ENOMEM;
+      give(&b);
+      if (b.p) {  // not taken (not a registered mapping): leave the pool as it is
+        b.release();
+        return BSG_OK;
+      }
+    }
+  }
+
+ private:
+  static constexpr size_t kMaxFree = 16;  // at most 1 GiB of idle pinned staging
+  std::mutex mu_;
+  std::vector<PinBuf> free_;
+};
+
 struct Stage {
   PinBuf buf;                // DMA staging (PinBuf::dma_only)
   hipEvent_t ev = nullptr;   // recorded after the H2D that reads the stage
@@ -767,7 +821,8 @@ struct bsg_ctx {
       t.eng = nullptr;
     }
     for (Stage& st : stages) {
-      st.buf.release();
+      if (st.ev) (void)hipEventSynchronize(st.ev);
+      StagePool::get().give(&st.buf);
       if (st.ev) (void)hipEventDestroy(st.ev);
       st.ev = nullptr;
     }
@@ -904,6 +959,13 @@ struct bsg_ctx {
     const size_t have = std::min(st.buf.cap, full);
     if (have >= want) return BSG_OK;
     const size_t nc = big ? full : std::min(full, std::max(want, 2 * have));
+    PinBuf pooled;
+    if (nc >= kStageMax && StagePool::get().take(&pooled)) {  // a pinned stage from the pool
+      if (sfill) std::memcpy(pooled.p, st.buf.p, sfill);
+      st.buf.release();
+      st.buf = pooled;
+      return BSG_OK;
+    }
     HCHECK(st.buf.grow(nc, sfill));
     return BSG_OK;
   }
@@ -1133,6 +1195,7 @@ struct bsg_ctx {
     for (Stage& st : stages) {
       if (st.inflight) HCHECK(hipEventSynchronize(st.ev));
       st.inflight = false;
+      StagePool::get().give(&st.buf);  // full-size stages go back to the process-wide pool
     }
     inflight.clear();
     ready.clear();
@@ -1252,6 +1315,8 @@ int bsg_init(int device) {
   bsg_engine_destroy(eng);
   if (rc) return rc;
   bsg::parallel_for(bsg::copy_threads(), [](size_t) {});  // the host copy pool's threads
+  // a ring's worth of full-size pinned stages for the first large stream
+  if ((rc = StagePool::get().fill(kStages))) return rc;
   // the streaming path once (registered staging, H2D from it, kernels writing into mapped
   // host memory, events): first uses the process would otherwise pay in its first Writer
   bsg_ctx* c = bsg_open(device, nullptr, nullptr, &rc);
