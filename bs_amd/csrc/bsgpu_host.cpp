@@ -960,7 +960,8 @@ struct bsg_ctx {
     if (have >= want) return BSG_OK;
     const size_t nc = big ? full : std::min(full, std::max(want, 2 * have));
     PinBuf pooled;
-    if (nc >= kStageMax && StagePool::get().take(&pooled)) {  // a pinned stage from the pool
+    // a full-size stage already pinned in the pool beats pinning a new one of any size
+    if (full == kStageMax && StagePool::get().take(&pooled)) {
       if (sfill) std::memcpy(pooled.p, st.buf.p, sfill);
       st.buf.release();
       st.buf = pooled;
