@@ -1,7 +1,7 @@
 """A/B of library builds on the host-memory paths: for each library (BSG_LIB_PATH), in a fresh
 process, 5 repetitions of (a) the C++ split.Writer -> store/mem on a 4 GiB stream in 32 MiB
 Writes and (b) the raw bsg_write/bsg_drain streaming of the same bytes; libraries alternate
-twice so box drift shows.   python tools/writer_ab.py lib_a.so lib_b.so ..."""
+twice (AB_ROUNDS) so box drift shows.   python tools/writer_ab.py lib_a.so lib_b.so ..."""
 import json
 import os
 import subprocess
@@ -53,7 +53,7 @@ def main():
         child()
         return
     libs = [os.path.abspath(x) for x in sys.argv[1:]]
-    for rnd in range(2):
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "2"))):
         for lib in libs:
             env = dict(os.environ, AB_CHILD="1", BSG_LIB_PATH=lib, BSG_LIB_PARTIAL="1")
             r = subprocess.run([sys.executable, __file__], env=env, capture_output=True, text=True,
