@@ -712,6 +712,10 @@ class StagePool {
     return *p;
   }
   bool take(PinBuf* out) {  // out: empty
+#ifdef BSG_NO_STAGE_POOL  // experiment switch (tools/writer_ab.py): every context pins its own
+    (void)out;
+    return false;
+#endif
     std::lock_guard<std::mutex> g(mu_);
     if (free_.empty()) return false;
     *out = free_.back();
@@ -720,7 +724,11 @@ class StagePool {
   }
   void give(PinBuf* b) {  // takes b's buffer if it is a full-size one; b is empty afterwards
     if (!b->p) return;
+#ifdef BSG_NO_STAGE_POOL
+    if (false) {
+#else
     if (b->cap >= kStageMax && b->map_len) {
+#endif
       std::lock_guard<std::mutex> g(mu_);
       if (free_.size() < kMaxFree) {
         free_.push_back(*b);
@@ -732,6 +740,10 @@ class StagePool {
     b->release();
   }
   int fill(int n) {  // bsg_init: make sure n full-size stages are pinned and waiting
+#ifdef BSG_NO_STAGE_POOL
+    (void)n;
+    return BSG_OK;
+#endif
     for (;;) {
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -1317,7 +1329,9 @@ int bsg_init(int device) {
   if (rc) return rc;
   bsg::parallel_for(bsg::copy_threads(), [](size_t) {});  // the host copy pool's threads
   // a ring's worth of full-size pinned stages for the first large stream
+#ifndef BSG_NO_INIT_STAGES  // experiment switch: no stages pinned ahead
   if ((rc = StagePool::get().fill(kStages))) return rc;
+#endif
   // the streaming path once (registered staging, H2D from it, kernels writing into mapped
   // host memory, events): first uses the process would otherwise pay in its first Writer
   bsg_ctx* c = bsg_open(device, nullptr, nullptr, &rc);

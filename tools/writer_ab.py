@@ -11,7 +11,21 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def node_cpus(node: int):
+    cpus = set()
+    for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def cpu_now() -> int:
+    return int(open("/proc/self/stat").read().rsplit(")", 1)[1].split()[36])
+
+
 def child():
+    if os.environ.get("AB_NODE"):  # bind the process (and so its first-touch memory) to a node
+        os.sched_setaffinity(0, node_cpus(int(os.environ["AB_NODE"])) & os.sched_getaffinity(0))
     sys.path.insert(0, ROOT)
     from bs_amd import bsgpu
     from bs_amd.synth import splitmix_array
@@ -23,7 +37,10 @@ def child():
     n = int(os.environ.get("AB_MIB", "4096")) << 20
     data = splitmix_array(2, n)
     mv = memoryview(data)
-    out = {"lib": os.environ["BSG_LIB_PATH"], "writer": [], "raw": []}
+    out = {"lib": os.path.basename(os.environ["BSG_LIB_PATH"]), "writer": [], "raw": [],
+           "cpus": sorted(os.sched_getaffinity(0))[:1] + [len(os.sched_getaffinity(0))],
+           "numa_nodes": len([d for d in os.listdir("/sys/devices/system/node")
+                              if d.startswith("node")]) if os.path.isdir("/sys/devices/system/node") else None}
     for rep in range(5):
         st = bsgpu.MemStore()
         t0 = time.perf_counter()
@@ -45,6 +62,8 @@ def child():
         sp.drain()
         out["raw"].append(round(n / (time.perf_counter() - t0) / 2**30, 2))
     sp.free()
+    out["cpu_end"] = cpu_now()
+    out["node"] = os.environ.get("AB_NODE")
     print(json.dumps(out), flush=True)
 
 
