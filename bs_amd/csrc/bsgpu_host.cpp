@@ -8,7 +8,11 @@
 // host; bsg_engine_finish() is the only synchronisation (and the place where a too-small
 // candidate buffer is grown and the run repeated).
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -118,6 +122,7 @@ struct PinBuf {
       void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
       if (m != MAP_FAILED) {
         (void)::madvise(m, n, MADV_HUGEPAGE);
+        bsg::numa_place(m, n);  // registering faults the pages in: on the device's node
         if (hipHostRegister(m, n, hipHostRegisterDefault) == hipSuccess) {
           *q = m;
           *len = n;
@@ -611,6 +616,9 @@ class CopyPool {
   explicit CopyPool(int workers) {
     for (int i = 0; i < workers; ++i) th_.emplace_back([this] { Work(); });
   }
+  void Bind(const cpu_set_t& cpus) {
+    for (std::thread& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus, &cpus);
+  }
   void Run(size_t n, const std::function<void(size_t)>& fn) {
     auto job = std::make_shared<PoolJob>();
     job->fn = &fn;
@@ -654,6 +662,12 @@ class CopyPool {
   std::deque<std::shared_ptr<PoolJob>> q_;
   std::vector<std::thread> th_;
 };
+
+CopyPool* copy_pool() {
+  // never destroyed: its workers stay blocked on the queue until the process exits
+  static CopyPool* pool = copy_threads() > 1 ? new CopyPool(copy_threads() - 1) : nullptr;
+  return pool;
+}
 }  // namespace
 
 void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
@@ -662,9 +676,85 @@ void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
     for (size_t i = 0; i < n; ++i) fn(i);
     return;
   }
-  // never destroyed: its workers stay blocked on the queue until the process exits
-  static CopyPool* pool = new CopyPool(copy_threads() - 1);
-  pool->Run(n, fn);
+  copy_pool()->Run(n, fn);
+}
+
+namespace {
+std::atomic<int> g_numa_node{-1};
+
+// The NUMA node of a device's PCI function, from sysfs (-1: unknown, e.g. one-node hosts).
+int device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  char path[160];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+
+// The CPUs of `node` this process may run on (false if none, or the node is unknown).
+bool node_cpus(int node, cpu_set_t* out) {
+  char path[96];
+  std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) {
+    std::fclose(f);
+    return false;
+  }
+  CPU_ZERO(out);
+  int a, b, n = 0;
+  while (std::fscanf(f, "%d", &a) == 1) {
+    b = a;
+    int c = std::fgetc(f);
+    if (c == '-') {
+      if (std::fscanf(f, "%d", &b) != 1) break;
+      c = std::fgetc(f);
+    }
+    for (int k = a; k <= b && k < CPU_SETSIZE; ++k)
+      if (CPU_ISSET(k, &allowed)) {
+        CPU_SET(k, out);
+        ++n;
+      }
+    if (c != ',') break;
+  }
+  std::fclose(f);
+  return n > 0;
+}
+}  // namespace
+
+void numa_setup(int device) {
+  static std::once_flag once;
+  std::call_once(once, [device] {
+    const char* e = std::getenv("BSG_NUMA");
+    if (!e || std::atoi(e) == 0) return;  // opt-in: measured no gain on the MI355X box
+    const int node = device_numa_node(device);
+    cpu_set_t cpus;
+    if (node < 0 || !node_cpus(node, &cpus)) return;
+    g_numa_node.store(node);
+    if (CopyPool* pool = copy_pool()) pool->Bind(cpus);
+    if (std::getenv("BSG_DEBUG_NUMA"))
+      std::fprintf(stderr, "bsgpu: device %d on NUMA node %d (%d CPUs)\n", device, node,
+                   CPU_COUNT(&cpus));
+  });
+}
+
+void numa_place(void* p, size_t len) {
+  const int node = g_numa_node.load();
+  if (node < 0 || node >= 64 || !p || !len) return;
+  const unsigned long mask = 1ul << node;
+  constexpr int kMpolPreferred = 1;  // numaif.h MPOL_PREFERRED (no libnuma dependency)
+  (void)syscall(SYS_mbind, p, len, kMpolPreferred, &mask, 64ul, 0u);
 }
 
 }  // namespace bsg
@@ -1277,6 +1367,7 @@ void bsg_default_table(uint32_t out[256]) { std::memcpy(out, kBuzhash32Seed1, 10
 int bsg_init(int device) {
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
   HCHECK(hipSetDevice(device));
+  bsg::numa_setup(device);
   // streams for the pool: one per hardware queue the process gets (GPU_MAX_HW_QUEUES, 4), the
   // ones a streaming context, a hasher and a batch engine take first
   constexpr int kWarmStreams = 4;
@@ -1565,6 +1656,7 @@ bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, i
     *err = BSG_ENODEV;
     return nullptr;
   }
+  bsg::numa_setup(device);
   bsg_ctx* c = new (std::nothrow) bsg_ctx();
   if (!c) {
     *err = BSG_ENOMEM;
@@ -1955,6 +2047,7 @@ extern "C" {
 bsg_hasher* bsg_hasher_new(int device) {
   if (device < 0 || device >= bsg_device_count() || hipSetDevice(device) != hipSuccess)
     return nullptr;
+  bsg::numa_setup(device);
   bsg_hasher* h = new (std::nothrow) bsg_hasher();
   if (!h) return nullptr;
   h->dev = device;

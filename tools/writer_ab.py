@@ -64,6 +64,8 @@ def child():
     sp.free()
     out["cpu_end"] = cpu_now()
     out["node"] = os.environ.get("AB_NODE")
+    out["env"] = {k: v for k, v in os.environ.items() if k.startswith("BSG_") and k not in
+                  ("BSG_LIB_PATH", "BSG_LIB_PARTIAL")}
     print(json.dumps(out), flush=True)
 
 
@@ -71,13 +73,19 @@ def main():
     if os.environ.get("AB_CHILD") == "1":
         child()
         return
-    libs = [os.path.abspath(x) for x in sys.argv[1:]]
+    # each argument: a library, optionally with environment settings for it: lib.so:K=V,K2=V2
+    specs = []
+    for x in sys.argv[1:]:
+        lib, _, kv = x.partition(":")
+        specs.append((os.path.abspath(lib), dict(p.split("=", 1) for p in kv.split(",") if p)))
     for rnd in range(int(os.environ.get("AB_ROUNDS", "2"))):
-        for lib in libs:
-            env = dict(os.environ, AB_CHILD="1", BSG_LIB_PATH=lib, BSG_LIB_PARTIAL="1")
+        for lib, extra in specs:
+            env = dict(os.environ, AB_CHILD="1", BSG_LIB_PATH=lib, BSG_LIB_PARTIAL="1", **extra)
             r = subprocess.run([sys.executable, __file__], env=env, capture_output=True, text=True,
                                timeout=600)
             sys.stdout.write(r.stdout if r.returncode == 0 else f"{lib} failed: {r.stderr[-1500:]}\n")
+            if r.returncode == 0 and "bsgpu:" in r.stderr:
+                sys.stdout.write("".join(l + "\n" for l in r.stderr.splitlines() if "bsgpu:" in l))
             sys.stdout.flush()
             if r.returncode:
                 sys.exit(r.returncode)
