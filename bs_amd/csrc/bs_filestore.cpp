@@ -91,7 +91,10 @@ std::string FileStore::BlobPath(const Ref& ref) const {  // file.go:33-40
 }
 
 FileStore::~FileStore() {
-  (void)FlushAll();
+  const Status s0 = FlushAll();  // group 0's error, which FlushAll reports (and clears)
+  if (!s0.ok())
+    std::fprintf(stderr, "bs::FileStore(%s): unreported write error (group 0): %s\n",
+                 root_.c_str(), s0.msg.c_str());
   {
     std::lock_guard<std::mutex> g(wb_mu_);
     wb_stop_ = true;
@@ -214,11 +217,16 @@ Status FileStore::Flush(uint64_t group) {
   std::unique_lock<std::mutex> g(wb_mu_);
   auto it = groups_.find(group);
   if (it == groups_.end()) return Status::Err(BSG_EINVAL, "unknown write group");
-  wb_done_cv_.wait(g, [&] { return groups_[group].outstanding == 0; });
-  Group& gr = groups_[group];
-  Status s = gr.err;
-  gr.err = Status::Ok();  // reported once
-  if (gr.closed && group != 0) groups_.erase(group);
+  // (a closed group with nothing outstanding and no error is erased by the last worker)
+  wb_done_cv_.wait(g, [&] {
+    auto i = groups_.find(group);
+    return i == groups_.end() || i->second.outstanding == 0;
+  });
+  it = groups_.find(group);
+  if (it == groups_.end()) return Status::Ok();
+  Status s = it->second.err;
+  it->second.err = Status::Ok();  // reported once
+  if (it->second.closed && group != 0) groups_.erase(it);
   return s;
 }
 
