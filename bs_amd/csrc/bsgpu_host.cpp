@@ -564,12 +564,14 @@ struct bsg_engine {
 };
 
 // ------------------------------------------------------------------------------------------
-// Streaming split.Writer (bsg_open / bsg_write / bsg_close / bsg_drain): a pipeline of kSlots
-// tiles, each with its own engine (HIP stream + work buffers), device slot and pinned staging.
+// Streaming split.Writer (bsg_open / bsg_write / bsg_close / bsg_drain): a pipeline of tiles.
+// Tile i's bytes go through a ring of pinned stages, by H2D on the context's copy stream, into
+// data slot i mod ndata; its kernels run on engine slot i mod nslots (HIP stream + work buffers).
 //
-//   host:  copy Write()s into staging[i] ... submit tile i ... copy into staging[i+1] ...
-//   slot:  [carry area kCarryCap | tile bytes | read slack]
-//   GPU :  H2D(i) -> scan/select(i) -> sel_ev(i) -> k_sha(i) -> D2H records(i)
+//   host:    copy Write()s into stage s ... flush s (H2D) ... stage s+1 ... submit tile i ...
+//   data:    [carry area kCarryCap | tile bytes | read slack]
+//   copies:  H2D(i, stage 0..3) -> copied_ev(i)      (waits for data slot i's previous tile)
+//   engine:  wait copied_ev(i) -> scan/select(i) -> sel_ev(i) -> k_sha(i) -> records(i)
 //
 // Tile i+1 needs from tile i only where its open chunk starts, which is known at sel_ev(i), a
 // fraction of a millisecond into tile i: the open chunk's bytes (at most kCarryCap; k_sha
@@ -770,11 +772,29 @@ int default_slots() {
   return std::max(2, std::min(kMaxSlots, v));
 }
 
+// Device copies of the tiles' bytes, decoupled from the engines: tile i's bytes go to data slot
+// i mod ndata and its kernels run on engine slot i mod nslots. With one more data slot than
+// engines, tile i's H2D does not wait for tile i - nslots' k_sha (which still reads that engine's
+// previous tile), only for tile i - ndata's: the copies run back to back on their own stream
+// while the chains of earlier tiles finish.
+constexpr int kMaxData = 8;
+int default_data_slots(int nslots) {
+  const char* e = std::getenv("BSG_DATA_SLOTS");
+  const int v = e ? std::atoi(e) : nslots + 1;
+  return std::max(std::max(2, nslots), std::min(kMaxData, v));
+}
+
+struct DataSlot {
+  DevBuf dbuf;                  // carry area + tile + slack
+  hipEvent_t free_ev = nullptr; // recorded on an engine stream after the last reader of dbuf
+  bool free_pending = false;    // free_ev recorded, not yet waited for by the copy stream
+};
+
 struct TileSlot {
   bsg_engine* eng = nullptr;  // created at the slot's first tile (a small stream needs one)
-  DevBuf dbuf;            // carry area + tile + slack
   PinBuf recs;            // records, D2H'd after k_sha
-  hipEvent_t h2d_ev = nullptr, done_ev = nullptr;
+  hipEvent_t h2d_ev = nullptr, done_ev = nullptr, copied_ev = nullptr;
+  int dslot = 0;          // data slot of the tile using this engine
   // state of the tile currently using the slot
   bool busy = false;          // submitted, records not yet collected
   bool sel_read = false;      // selection snapshot consumed (open_next / nchunks known)
@@ -871,6 +891,11 @@ struct bsg_ctx {
   uint64_t carry_cap = kDefaultCarryCap;
   int nslots = default_slots();
   TileSlot slots[kMaxSlots];
+  int ndata = default_data_slots(nslots);
+  DataSlot data[kMaxData];
+  int dcur = 0;             // data slot of the tile the host is filling
+  bool dready = false;      // the copy stream waits for data[dcur]'s previous readers already
+  hipStream_t cstream = nullptr;  // H2D copies of every tile (from the process's stream pool)
   Stage stages[kStages];
   int cur = 0;              // slot of the tile the host is filling
   size_t fill = 0;          // bytes of the current tile (copied to the device or staged)
@@ -908,20 +933,44 @@ struct bsg_ctx {
     t.eng->snapshot = true;
     HCHECK(hipEventCreateWithFlags(&t.h2d_ev, hipEventDisableTiming));
     HCHECK(hipEventCreateWithFlags(&t.done_ev, hipEventDisableTiming));
+    HCHECK(hipEventCreateWithFlags(&t.copied_ev, hipEventDisableTiming));
+    return BSG_OK;
+  }
+
+  // data[dcur] ready to receive the current tile's bytes on the copy stream: allocated, and
+  // ordered after the kernels of the tile that used it last.
+  int copy_prepare() {
+    if (!cstream) HCHECK(stream_acquire(dev, &cstream));
+    DataSlot& ds = data[dcur];
+    HCHECK(ds.dbuf.ensure(carry_cap + tile + kReadSlack));
+    if (!ds.free_ev) HCHECK(hipEventCreateWithFlags(&ds.free_ev, hipEventDisableTiming));
+    if (!dready) {
+      if (ds.free_pending) HCHECK(hipStreamWaitEvent(cstream, ds.free_ev, 0));
+      ds.free_pending = false;
+      dready = true;
+    }
     return BSG_OK;
   }
 
   void release() {
     (void)hipSetDevice(dev);
+    if (cstream) (void)hipStreamSynchronize(cstream);
     for (TileSlot& t : slots) {
       if (t.eng) (void)hipStreamSynchronize(t.eng->stream);
-      t.dbuf.release();
       t.recs.release();
       if (t.h2d_ev) (void)hipEventDestroy(t.h2d_ev);
       if (t.done_ev) (void)hipEventDestroy(t.done_ev);
+      if (t.copied_ev) (void)hipEventDestroy(t.copied_ev);
       bsg_engine_destroy(t.eng);
       t.eng = nullptr;
     }
+    for (DataSlot& ds : data) {
+      ds.dbuf.release();
+      if (ds.free_ev) (void)hipEventDestroy(ds.free_ev);
+      ds.free_ev = nullptr;
+    }
+    if (cstream) stream_release(dev, cstream);
+    cstream = nullptr;
     for (Stage& st : stages) {
       if (st.ev) (void)hipEventSynchronize(st.ev);
       StagePool::get().give(&st.buf);
@@ -1026,19 +1075,17 @@ struct bsg_ctx {
     return BSG_OK;
   }
 
-  // Copy the staged bytes of the current tile to its device slot (on the slot's engine stream,
-  // behind that slot's previous tile) and move to the next stage.
+  // Copy the staged bytes of the current tile to its data slot (on the copy stream) and move to
+  // the next stage.
   int flush_stage() {
     if (sfill == 0) return BSG_OK;
-    int rc = ensure_slot(cur);
+    int rc = copy_prepare();
     if (rc) return rc;
-    TileSlot& t = slots[cur];
-    HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
     Stage& st = stages[scur];
     tail_append(st.buf.as<uint8_t>(), sfill);  // history for the next tile
-    HCHECK(hipMemcpyAsync(t.dbuf.as<uint8_t>() + carry_cap + (fill - sfill), st.buf.p, sfill,
-                          hipMemcpyHostToDevice, t.eng->stream));
-    HCHECK(hipEventRecord(st.ev, t.eng->stream));
+    HCHECK(hipMemcpyAsync(data[dcur].dbuf.as<uint8_t>() + carry_cap + (fill - sfill), st.buf.p,
+                          sfill, hipMemcpyHostToDevice, cstream));
+    HCHECK(hipEventRecord(st.ev, cstream));
     st.inflight = true;
     scur = (scur + 1) % kStages;
     sfill = 0;
@@ -1087,8 +1134,11 @@ struct bsg_ctx {
     // buffers are reused (the H2Ds above already queue behind its kernels on the same stream)
     rc0 = reclaim(i);
     if (rc0) return rc0;
-    HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
-    uint8_t* base = t.dbuf.as<uint8_t>();
+    if ((rc0 = copy_prepare())) return rc0;
+    // the tile's kernels (and the carry copy into its data slot) run after its H2D copies
+    HCHECK(hipEventRecord(t.copied_ev, cstream));
+    HCHECK(hipStreamWaitEvent(e->stream, t.copied_ev, 0));
+    uint8_t* base = data[dcur].dbuf.as<uint8_t>();
     StreamDesc d{};
     d.data_off = carry_cap;
     d.len = fill;
@@ -1107,8 +1157,8 @@ struct bsg_ctx {
       if (carry <= pt.eng->descs[0].carry_cap) {  // bytes carried on the device
         if (carry) {
           // the open chunk may itself have started in front of pt's tile (carried into it)
-          const uint8_t* src =
-              pt.dbuf.as<uint8_t>() + (int64_t)carry_cap + ((int64_t)open - (int64_t)pt.seg_base);
+          const uint8_t* src = data[pt.dslot].dbuf.as<uint8_t>() + (int64_t)carry_cap +
+                               ((int64_t)open - (int64_t)pt.seg_base);
           HCHECK(hipMemcpyAsync(base + carry_cap - carry, src, carry, hipMemcpyDeviceToDevice,
                                 e->stream));
           // the previous slot must not be overwritten before this copy has read it
@@ -1130,6 +1180,11 @@ struct bsg_ctx {
       // the previous tile's records can be fetched as soon as its k_sha is done
       rc = enqueue_recs(prev);
       if (rc) return rc;
+      // the previous tile's data slot is free once its kernels (and the carry copy above, which
+      // its stream now waits for) are done: the copy stream waits for this before refilling it
+      DataSlot& pd = data[pt.dslot];
+      HCHECK(hipEventRecord(pd.free_ev, pt.eng->stream));
+      pd.free_pending = true;
     }
     e->d_data = base;
     e->descs.assign(1, d);
@@ -1143,6 +1198,9 @@ struct bsg_ctx {
     t.final_seg = final_seg;
     t.seg_base = pos;
     t.len = fill;
+    t.dslot = dcur;
+    dcur = (dcur + 1) % ndata;
+    dready = false;
     inflight.push_back(i);
     std::memcpy(hist, tail, 64);  // window history for the next tile
     pos += fill;
@@ -1205,15 +1263,13 @@ struct bsg_ctx {
       }
       int rc = flush_stage();  // staged bytes of this tile go first (offsets stay in order)
       if (rc) return rc;
-      if ((rc = ensure_slot(cur))) return rc;
-      TileSlot& t = slots[cur];
-      HCHECK(t.dbuf.ensure(carry_cap + tile + kReadSlack));
+      if ((rc = copy_prepare())) return rc;
       const size_t k = std::min(n, tile - fill);
       const size_t staged = fill + k == tile ? std::min<size_t>(k, 4096) : 0;
       const size_t direct = k - staged;
       if (direct) {
-        HCHECK(hipMemcpyAsync(t.dbuf.as<uint8_t>() + carry_cap + fill, q, direct,
-                              hipMemcpyHostToDevice, t.eng->stream));
+        HCHECK(hipMemcpyAsync(data[dcur].dbuf.as<uint8_t>() + carry_cap + fill, q, direct,
+                              hipMemcpyHostToDevice, cstream));
         tail_append(q, direct);
         fill += direct;
       }
@@ -1288,6 +1344,10 @@ struct bsg_ctx {
   // discarded, also after a device error (Counters::error is per run: the buffers stay valid).
   // Only a failing HIP call (a real fault) leaves the context unusable: bsg_free it.
   int reset() {
+    if (cstream) HCHECK(hipStreamSynchronize(cstream));
+    for (DataSlot& ds : data) ds.free_pending = false;
+    dcur = 0;
+    dready = false;
     for (int k = 0; k < nslots; ++k) {
       TileSlot& t = slots[k];
       if (t.eng) HCHECK(hipStreamSynchronize(t.eng->stream));
