@@ -242,8 +242,8 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     w.free()
     return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "chunks": nch,
             "path": "host memory -> bsg_write (ring of 4 x 64 MiB pinned stages, each copied "
-                    "H2D as it fills) -> split + SHA-256 -> records in host memory; tile 256 MiB, "
-                    "3 tiles in flight"}
+                    "H2D as it fills, on a copy stream into 4 device data slots) -> split + "
+                    "SHA-256 on 3 engines -> records in host memory; tile 256 MiB"}
 
 
 # rocprofv3 names of each stage's kernels (k_sha: two instantiations launched back to back, one of
