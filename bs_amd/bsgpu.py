@@ -71,6 +71,8 @@ def lib() -> ctypes.CDLL:
         "bsg_open": (vp, [ctypes.c_int, ctypes.POINTER(Params), u32p, ctypes.POINTER(ctypes.c_int)]),
         "bsg_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
         "bsg_close": (ctypes.c_int, [vp]),
+        "bsg_close_begin": (ctypes.c_int, [vp]),
+        "bsg_close_step": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_size_t)]),
         "bsg_pending": (ctypes.c_size_t, [vp]),
         "bsg_drain": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
         "bsg_set_tile": (ctypes.c_int, [vp, ctypes.c_size_t]),
@@ -445,6 +447,15 @@ class StreamingSplitter:
 
     def close(self) -> None:
         _check(lib().bsg_close(self.h), "bsg_close")
+
+    def close_steps(self):
+        """bsg_close_begin, then one bsg_close_step per tile still on the device; yields the
+        chunks each step made drainable (their concatenation is what close() + drain() give)."""
+        _check(lib().bsg_close_begin(self.h), "bsg_close_begin")
+        left = ctypes.c_size_t(1)
+        while left.value:
+            _check(lib().bsg_close_step(self.h, ctypes.byref(left)), "bsg_close_step")
+            yield self.drain()
 
     def reset(self) -> None:
         _check(lib().bsg_reset(self.h), "bsg_reset")

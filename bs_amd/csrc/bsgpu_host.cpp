@@ -179,28 +179,37 @@ int herr(hipError_t e) { return e == hipSuccess ? BSG_OK : BSG_EDEVICE; }
 // an engine per tile slot paid every time. Streams go back to the pool instead.
 constexpr size_t kStreamPoolMax = 32;
 std::mutex g_stream_mu;
-std::vector<hipStream_t>& stream_pool(int device) {
-  static auto* pools = new std::vector<std::vector<hipStream_t>>(64);  // never destroyed
-  return (*pools)[(size_t)device & 63];
+// `prio`: a separate pool of streams at the device's greatest priority (the runtime gives them
+// hardware queues of their own), for short synchronous work that must not wait in a queue
+// behind a long k_sha (the split::Writer's tree-node hashes).
+std::vector<hipStream_t>& stream_pool(int device, bool prio) {
+  static auto* pools = new std::vector<std::vector<hipStream_t>>(128);  // never destroyed
+  return (*pools)[((size_t)device & 63) * 2 + (prio ? 1 : 0)];
 }
-hipError_t stream_acquire(int device, hipStream_t* s) {
+hipError_t stream_acquire(int device, hipStream_t* s, bool prio = false) {
   {
     std::lock_guard<std::mutex> g(g_stream_mu);
-    auto& v = stream_pool(device);
+    auto& v = stream_pool(device, prio);
     if (!v.empty()) {
       *s = v.back();
       v.pop_back();
       return hipSuccess;
     }
   }
+  if (prio) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+    (void)hipGetLastError();
+  }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 // The stream must be idle (callers synchronise it first); the device must be current.
-void stream_release(int device, hipStream_t s) {
+void stream_release(int device, hipStream_t s, bool prio = false) {
   if (!s) return;
   {
     std::lock_guard<std::mutex> g(g_stream_mu);
-    auto& v = stream_pool(device);
+    auto& v = stream_pool(device, prio);
     if (v.size() < kStreamPoolMax) {
       v.push_back(s);
       return;
@@ -1376,20 +1385,24 @@ struct bsg_ctx {
     return BSG_OK;
   }
 
-  int close() {
+  int close_begin() {
     if (fill == 0 && pos == 0) return BSG_OK;  // empty stream: no chunks
     // The final segment must hold at least one byte: the open chunk's flush is emitted by the
     // scan of its last strip. write() and window() never submit a tile without leaving bytes
     // behind, so this cannot happen; fail loudly rather than drop the last chunk.
     if (fill == 0) return BSG_ESTATE;
-    int rc = submit(true);
-    if (rc) return rc;
-    while (!inflight.empty()) {
-      bool got = false;
-      rc = collect_front(true, &got);
-      if (rc) return rc;
-    }
-    return BSG_OK;
+    return submit(true);
+  }
+  int close_step(size_t* left) {  // the oldest tile on the device: wait, collect its records
+    bool got = false;
+    int rc = collect_front(true, &got);
+    *left = inflight.size();
+    return rc;
+  }
+  int close() {
+    int rc = close_begin();
+    for (size_t left = inflight.size(); rc == BSG_OK && left;) rc = close_step(&left);
+    return rc;
   }
 };
 
@@ -1814,6 +1827,29 @@ int bsg_close(bsg_ctx* c) {
   return rc;
 }
 
+int bsg_close_begin(bsg_ctx* c) {
+  if (!c) return BSG_EINVAL;
+  if (c->closed) return c->sticky;
+  c->closed = true;
+  if (c->sticky) return c->sticky;
+  if (hipSetDevice(c->dev) != hipSuccess) return c->sticky = BSG_EDEVICE;
+  int rc = c->close_begin();
+  if (rc) c->sticky = rc;
+  return rc;
+}
+
+int bsg_close_step(bsg_ctx* c, size_t* left) {
+  if (!c || !left) return BSG_EINVAL;
+  *left = 0;
+  if (!c->closed) return BSG_ESTATE;
+  if (c->sticky) return c->sticky;
+  if (c->inflight.empty()) return BSG_OK;
+  if (hipSetDevice(c->dev) != hipSuccess) return c->sticky = BSG_EDEVICE;
+  int rc = c->close_step(left);
+  if (rc) c->sticky = rc;
+  return rc;
+}
+
 size_t bsg_pending(const bsg_ctx* c) {
   if (!c) return 0;
   bsg_ctx* m = const_cast<bsg_ctx*>(c);  // polling completed tiles is not a visible change
@@ -2015,8 +2051,10 @@ struct bsg_hasher {
   int dev = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
+  bool prio = false;  // stream from the high-priority pool (BSG_HASHER_PRIO)
   DevBuf data, off, len, refs;
   PinBuf h_meta;  // off[n] | len[n] staged for one H2D
+  PinBuf h_small; // a small batch's host bytes, then its refs: pinned, so both copies are DMA
   // Large batches (the verifying split.Reader, bsg_sha256_batch of many blobs): the blobs are
   // packed at 16-byte offsets into pinned staging and hashed by an engine in bsg_engine_hash
   // mode, whose wave-mode chains take the longest blobs (k_sha_blobs hashes one blob per lane,
@@ -2087,17 +2125,26 @@ struct bsg_hasher {
     HCHECK(h_meta.ensure(16ull * n));
     std::memcpy(h_meta.p, o, 8ull * n);
     std::memcpy(h_meta.as<uint8_t>() + 8ull * n, l, 8ull * n);
-    if (hi)
-      HCHECK(hipMemcpyAsync(data.p, base, hi,
-                            on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, stream));
+    // host bytes (tree nodes: pageable std::string) go through pinned memory, whose H2D / D2H
+    // are single DMAs instead of the runtime's chunked staging of pageable memory
+    HCHECK(h_small.ensure(std::max<uint64_t>(on_device ? 0 : hi, 32ull * n)));
+    if (hi) {
+      if (on_device) {
+        HCHECK(hipMemcpyAsync(data.p, base, hi, hipMemcpyDeviceToDevice, stream));
+      } else {
+        std::memcpy(h_small.p, base, hi);
+        HCHECK(hipMemcpyAsync(data.p, h_small.p, hi, hipMemcpyHostToDevice, stream));
+      }
+    }
     HCHECK(hipMemcpyAsync(off.p, h_meta.p, 8ull * n, hipMemcpyHostToDevice, stream));
     HCHECK(hipMemcpyAsync(len.p, h_meta.as<uint8_t>() + 8ull * n, 8ull * n,
                           hipMemcpyHostToDevice, stream));
     BlobShaArgs a{data.as<uint8_t>(), off.as<uint64_t>(), len.as<uint64_t>(), n,
                   refs.as<uint8_t>()};
     HCHECK(launch_sha_blobs(a, stream, num_cus));
-    HCHECK(hipMemcpyAsync(out, refs.p, 32ull * n, hipMemcpyDeviceToHost, stream));
+    HCHECK(hipMemcpyAsync(h_small.p, refs.p, 32ull * n, hipMemcpyDeviceToHost, stream));
     HCHECK(hipStreamSynchronize(stream));
+    std::memcpy(out, h_small.p, 32ull * n);
     return BSG_OK;
   }
 };
@@ -2112,7 +2159,12 @@ bsg_hasher* bsg_hasher_new(int device) {
   if (!h) return nullptr;
   h->dev = device;
   h->num_cus = device_cus(device);
-  if (stream_acquire(device, &h->stream) != hipSuccess) {
+  static const bool prio = [] {
+    const char* e = std::getenv("BSG_HASHER_PRIO");
+    return e && std::atoi(e) != 0;
+  }();
+  h->prio = prio;
+  if (stream_acquire(device, &h->stream, h->prio) != hipSuccess) {
     delete h;
     return nullptr;
   }
@@ -2160,10 +2212,11 @@ void bsg_hasher_free(bsg_hasher* h) {
   h->len.release();
   h->refs.release();
   h->h_meta.release();
+  h->h_small.release();
   h->stage.release();
   h->dstage.release();
   if (h->eng) bsg_engine_destroy(h->eng);
-  if (h->stream) stream_release(h->dev, h->stream);
+  if (h->stream) stream_release(h->dev, h->stream, h->prio);
   delete h;
 }
 

@@ -263,7 +263,16 @@ class Writer {
 
  private:
   explicit Writer(int device);
-  Status Drain();
+  Status Drain();                                   // take and process, on this thread
+  size_t TakeRecords(std::vector<bsg_chunk>* out);  // completed chunk records from the context
+  Status Process(const std::vector<bsg_chunk>& recs);  // Put + TreeBuilder.Add, stream order
+  // A Write's records are processed on a background thread while the Write copies its bytes
+  // (the copy waits on the H2D copies; processing is host bookkeeping): Submit hands records
+  // over, Join waits for them and returns the first error.
+  struct Bg;
+  std::unique_ptr<Bg> bg_;
+  void Submit(std::vector<bsg_chunk>* recs);
+  Status Join();
   Status Add(const Ref& ref, uint64_t len, unsigned level);  // hashsplit TreeBuilder.Add
   Status F(TBNode& n, std::shared_ptr<Wrapped>* out);        // split.go:52-81
   Status PutProto(const Node& node, Ref* ref);               // proto.go:22-29
@@ -295,6 +304,13 @@ class Writer {
   Ref root_{};
   bool closed_ = false;
   Status sticky_;
+  // where a Writer's time goes (seconds), printed when it is destroyed if BSG_DEBUG_WRITER is set
+  // (drain: records processed on the background thread, overlapping the copies; join: what the
+  // Writes waited for it)
+  struct Timing {
+    double copy = 0, drain = 0, join = 0, hash = 0, close = 0;
+    uint64_t hash_calls = 0;
+  } tm_;
 };
 
 // split.Protect (split/split.go:306-322), the gc.ProtectFunc for split trees: the children of

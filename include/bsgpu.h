@@ -105,14 +105,20 @@ int bsg_host_unregister(void* p);
 int bsg_write_pinned(bsg_ctx* ctx, const uint8_t* p, size_t n);
 /* Flushes the final chunk (hashsplit Splitter.Close). Idempotent. */
 int bsg_close(bsg_ctx* ctx);
+/* bsg_close in steps, so that a caller can Put the chunks of earlier tiles while the last ones
+ * finish: bsg_close_begin submits the final segment without waiting (the stream is closed);
+ * each bsg_close_step waits for the oldest tile still on the device and makes its chunks
+ * drainable, storing the number of tiles still on the device in *left (0: as after bsg_close). */
+int bsg_close_begin(bsg_ctx* ctx);
+int bsg_close_step(bsg_ctx* ctx, size_t* left);
 /* Number of finished chunks not yet drained, and drain up to cap of them (stream order). */
 size_t bsg_pending(const bsg_ctx* ctx);
 size_t bsg_drain(bsg_ctx* ctx, bsg_chunk* out, size_t cap);
 /* Device tile size in bytes (default 256 MiB); call before the first write. Three tiles are
- * in flight at once (BSG_STREAM_SLOTS overrides): tile i+1's split starts as soon as tile i's
+ * processed at once (BSG_STREAM_SLOTS overrides): tile i+1's split starts as soon as tile i's
  * boundaries are known, while tile i's SHA-256 is still running. Host bytes pass through a
- * ring of four pinned staging buffers of min(tile, 64 MiB), each copied to its tile's device
- * slot as soon as it is full. */
+ * ring of four pinned staging buffers of min(tile, 64 MiB), each copied to the device as soon
+ * as it is full, into one of four device data slots (BSG_DATA_SLOTS). */
 int bsg_set_tile(bsg_ctx* ctx, size_t tile_bytes);
 /* Longest open chunk carried between tiles as bytes on the device (default 8 MiB); a longer
  * one is carried as a SHA-256 midstate, which makes the next tile wait for this tile's hashes.

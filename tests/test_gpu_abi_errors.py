@@ -67,3 +67,34 @@ def test_persistent_hasher_batches(gpu):
                 [hashlib.sha256(b).digest() for b in blobs]
     finally:
         L.bsg_hasher_free(h)
+
+
+def test_close_in_steps(gpu, oracle, table):
+    """bsg_close_begin + bsg_close_step: the tiles still on the device finish one per step, and
+    the chunks of all steps are exactly those of bsg_close (the oracle's); a step before begin is
+    BSG_ESTATE, a step after the last returns 0 tiles left."""
+    import ctypes
+    from bs_amd.synth import splitmix_array
+    L = gpu.lib()
+    d = splitmix_array(77, (9 << 20) + 4321)
+    w = gpu.StreamingSplitter(bits=13, min_size=256, tile=1 << 20)
+    left = ctypes.c_size_t(5)
+    assert L.bsg_close_step(w.h, ctypes.byref(left)) == -71 and left.value == 0
+    got = []
+    for i in range(0, len(d), 3 << 20):
+        w.write(memoryview(d)[i:i + (3 << 20)])
+        got.append(w.drain())
+    steps = list(w.close_steps())
+    assert len(steps) >= 2                           # several tiles were still on the device
+    got += steps
+    assert L.bsg_close_step(w.h, ctypes.byref(left)) == 0 and left.value == 0
+    assert L.bsg_write(w.h, b"y", 1) == -71
+    w.free()
+    want = oracle.split(table, d, bits=13, min_size=256)
+    ch = np.concatenate(got)
+    assert len(ch) == len(want)
+    for f in ("offset", "len", "level", "ref"):
+        assert (ch[f] == want[f]).all(), f
+    e = gpu.StreamingSplitter()                      # an empty stream: nothing on the device
+    assert all(len(x) == 0 for x in e.close_steps())
+    e.free()
