@@ -108,3 +108,49 @@ def test_reader_verify_detects_corruption(gpu, tmp_path):
     with pytest.raises(gpu.BsgError) as ei:
         gpu.Reader(fs, root, verify=True).read_all()
     assert ei.value.code == gpu.CORRUPT
+
+
+@pytest.mark.parametrize("write_behind", [1 << 30, 1])
+def test_writer_put_failure_surfaces(gpu, tmp_path, oracle, table, write_behind):
+    """A chunk that store/file cannot write (its blobs/<hh> directory is a regular file) makes a
+    later Write or the Close fail, as a Put error inside split.Writer's F propagates out of
+    Write / Close in the reference (split/split.go:71-77, :104-126), and the Writer stays failed.
+    The chunks are Put on the Writer's background
+    thread while the next Write copies, so the error arrives one Write late or at Close."""
+    from bs_amd.synth import splitmix_array
+    data = splitmix_array(4242, 24 << 20).tobytes()
+    chunks = oracle.split(table, data)
+    bad = bytes(chunks[len(chunks) // 2]["ref"]).hex()
+    root = str(tmp_path)
+    os.makedirs(os.path.join(root, "blobs"), exist_ok=True)
+    with open(os.path.join(root, "blobs", bad[:2]), "wb") as f:
+        f.write(b"not a directory")
+    fs = gpu.FileStore(root)
+    fs.set_write_behind(write_behind)
+    w = gpu.Writer(fs, tile=1 << 20)
+    failed = None
+    for i in range(0, len(data), 1 << 20):
+        try:
+            w.write(data[i:i + (1 << 20)])
+        except gpu.BsgError as e:
+            failed = e
+            break
+    if failed is None:
+        with pytest.raises(gpu.BsgError):
+            w.close()
+    with pytest.raises(gpu.BsgError):    # sticky
+        w.write(b"x")
+    with pytest.raises(gpu.BsgError):
+        w.close()
+    w.free()
+    fs.free()  # waits for the write-behind queue
+    # every blob that did reach the disk is whole and named by its hash
+    n = 0
+    for dirpath, _, files in os.walk(os.path.join(root, "blobs")):
+        for name in files:
+            if len(name) != 64:
+                continue  # the blocking file
+            with open(os.path.join(dirpath, name), "rb") as f:
+                assert hashlib.sha256(f.read()).hexdigest() == name
+            n += 1
+    assert n > 0
