@@ -1441,10 +1441,17 @@ int bsg_init(int device) {
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
   HCHECK(hipSetDevice(device));
   bsg::numa_setup(device);
-  // streams for the pool: one per hardware queue the process gets (GPU_MAX_HW_QUEUES, 4), the
-  // ones a streaming context, a hasher and a batch engine take first
-  constexpr int kWarmStreams = 4;
-  hipStream_t s[kWarmStreams] = {};
+  // streams for the pool. The first four get the process's hardware queues (GPU_MAX_HW_QUEUES,
+  // 4); every further one still costs ~2.4 ms to create, and each live split::Writer holds
+  // three (its hasher's, its first engine's, its copy stream): a Writer opened while others are
+  // alive spent 7.5 of its 13 ms creating them (profiles/r03_fresh_ctx_api_trace.txt). So the
+  // pool starts with BSG_INIT_STREAMS of them (default 16: five live Writers' worth).
+  static const int kWarmStreams = [] {
+    const char* v = std::getenv("BSG_INIT_STREAMS");
+    const int n = v ? std::atoi(v) : 16;
+    return std::max(1, std::min<int>(n, (int)kStreamPoolMax));
+  }();
+  hipStream_t s[kStreamPoolMax] = {};
   int got = 0;
   hipError_t e = hipSuccess;
   for (; got < kWarmStreams && e == hipSuccess; ++got) e = stream_acquire(device, &s[got]);
