@@ -1,3 +1,10 @@
+"""Latency of the library's short calls after bsg_init (one JSON line): six 1 MiB split::Writers
+each opened while the earlier ones are still alive (each needs its own context, hasher and
+streams), three pooled ones, bsg_split_hash_batch of 64 x 256 KiB streams and bsg_sha256_batch of
+256 x 64 KiB blobs, six calls each (ms). BSG_INIT_STREAMS sets the warm stream pool.
+
+  python tools/live_writers.py
+"""
 import os, sys, time, json
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 from bs_amd import bsgpu
