@@ -302,6 +302,7 @@ struct bsg_engine {
       fidx, bnd_end, bnd_info, scount, last_end, out, carry, ctr, long_list, order, buckets, jinfo, jdesc,
       regions, oreg, rorder;
   PinBuf h_streams, h_strip0, h_ctr;
+  uint32_t htable[256];  // the table in `table` (a pooled batch engine may get another one)
   // Optional snapshot right after selection (streaming pipeline): the counters and every
   // stream's last chunk end land in pinned memory and sel_ev fires, long before k_sha ends.
   bool snapshot = false;
@@ -1545,9 +1546,9 @@ bsg_engine* bsg_engine_create(int device, const uint32_t* table, int* err) {
     return nullptr;
   }
   e->num_cus = device_cus(device);
+  std::memcpy(e->htable, table ? table : kBuzhash32Seed1, sizeof e->htable);
   if (e->table.ensure(1024) != hipSuccess ||
-      hipMemcpy(e->table.p, table ? table : kBuzhash32Seed1, 1024, hipMemcpyHostToDevice) !=
-          hipSuccess) {
+      hipMemcpy(e->table.p, e->htable, 1024, hipMemcpyHostToDevice) != hipSuccess) {
     bsg_engine_destroy(e);
     *err = BSG_EDEVICE;
     return nullptr;
@@ -1893,6 +1894,52 @@ void bsg_free(bsg_ctx* c) {
   delete c;
 }
 
+// bsg_split_hash_batch keeps a few engines (work buffers, pinned counters) for the next call:
+// creating and freeing one per call cost ~1 ms of allocations (profiles/r03_split_hash_batch_*).
+static std::mutex g_batch_eng_mu;
+static std::vector<bsg_engine*>& batch_engines() {
+  static auto* v = new std::vector<bsg_engine*>();  // never destroyed (see ctx_pool)
+  return *v;
+}
+static bsg_engine* batch_engine_take(int device, const uint32_t* table, int* rc) {
+  bsg_engine* e = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_batch_eng_mu);
+    auto& v = batch_engines();
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i]->dev == device) {
+        e = v[i];
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+  }
+  if (!e) return bsg_engine_create(device, table, rc);
+  *rc = BSG_OK;
+  const uint32_t* t = table ? table : kBuzhash32Seed1;
+  if (std::memcmp(e->htable, t, sizeof e->htable) != 0) {
+    std::memcpy(e->htable, t, sizeof e->htable);
+    if (hipSetDevice(device) != hipSuccess ||
+        hipMemcpy(e->table.p, e->htable, 1024, hipMemcpyHostToDevice) != hipSuccess) {
+      bsg_engine_destroy(e);
+      *rc = BSG_EDEVICE;
+      return nullptr;
+    }
+  }
+  return e;
+}
+static void batch_engine_give(bsg_engine* e, bool ok) {
+  if (ok && hipSetDevice(e->dev) == hipSuccess && hipStreamSynchronize(e->stream) == hipSuccess) {
+    e->retry_cap = 0;
+    std::lock_guard<std::mutex> g(g_batch_eng_mu);
+    if (batch_engines().size() < 2) {
+      batch_engines().push_back(e);
+      return;
+    }
+  }
+  (void)hipGetLastError();
+  bsg_engine_destroy(e);
+}
+
 int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* off,
                          const uint64_t* len, uint32_t nstreams, const bsg_params* params,
                          const uint32_t* table, bsg_chunk* out, uint64_t cap, uint64_t* counts,
@@ -1900,7 +1947,7 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
   if (nstreams && (!host_data || !off || !len)) return BSG_EINVAL;
   if (!out && cap) return BSG_EINVAL;
   int rc;
-  bsg_engine* e = bsg_engine_create(device, table, &rc);
+  bsg_engine* e = batch_engine_take(device, table, &rc);
   if (!e) return rc;
   // Runs of at most 65,535 streams (the engine's limit) and about 8 GiB of device bytes (a
   // larger stream goes alone); each run's streams are packed 16-byte aligned into one buffer.
@@ -1908,7 +1955,8 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
   constexpr uint64_t kRunBytes = 8ull << 30;
   constexpr uint64_t kPackWindow = 64ull << 20;
   DevBuf d;
-  PinBuf pack;
+  PinBuf pack;  // the packing window: a full-size stage from the process's pool when one is free
+  pack.dma_only = true;
   std::vector<uint64_t> doff;
   uint64_t n = 0;  // records of all runs so far (written to out while they fit in cap)
   for (uint32_t s0 = 0; s0 < nstreams && rc == BSG_OK;) {
@@ -1928,6 +1976,8 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
     // Streams shorter than the pinned window are packed at their device offsets into it and
     // copied a window at a time (one H2D for many small streams); longer ones directly.
     const uint64_t win = std::min<uint64_t>(total, kPackWindow);
+    static_assert(kPackWindow <= kStageMax, "a pooled stage holds the packing window");
+    if (win && !pack.p) (void)StagePool::get().take(&pack);
     if (win && pack.ensure(win) != hipSuccess) {
       rc = BSG_ENOMEM;
       break;
@@ -1971,8 +2021,8 @@ int bsg_split_hash_batch(int device, const uint8_t* host_data, const uint64_t* o
   }
   if (nchunks) *nchunks = n;
   d.release();
-  pack.release();
-  bsg_engine_destroy(e);
+  StagePool::get().give(&pack);  // keeps a full-size registered stage, frees anything else
+  batch_engine_give(e, rc == BSG_OK);
   return rc;
 }
 

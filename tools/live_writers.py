@@ -10,7 +10,7 @@ sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 from bs_amd import bsgpu
 from bs_amd.synth import splitmix_array
 bsgpu.init(0)
-tag = "init_streams=" + os.environ.get("BSG_INIT_STREAMS", "16")
+tag = os.environ.get("BSG_LIB_PATH", "default") + " init_streams=" + os.environ.get("BSG_INIT_STREAMS", "16")
 data = splitmix_array(1, 1 << 20)
 st = bsgpu.MemStore()
 ws, out = [], []
