@@ -454,3 +454,30 @@ def test_write_pinned_matches_oracle(gpu, oracle, table, tile, pieces):
     assert len(got) == len(ref)
     assert (got["offset"] == ref["offset"]).all() and (got["ref"] == ref["ref"]).all()
     assert (got["level"] == ref["level"]).all()
+
+
+def test_split_hash_batch_tables_interleaved_and_threads(gpu, oracle, table):
+    """bsg_split_hash_batch re-uses pooled engines: a call with another buzhash32 table (bsg_open's
+    and split_hash_batch's `table` argument) must not see the previous call's, whether calls
+    alternate on one thread or run on several at once. Random data, so every boundary depends on
+    the table; each result equals the oracle's under the same table."""
+    from concurrent.futures import ThreadPoolExecutor
+    from bs_amd.synth import splitmix_array
+    rng = np.random.default_rng(7)
+    tables = [table] + [rng.integers(0, 2**32, size=256, dtype=np.uint64).astype(np.uint32)
+                        for _ in range(2)]
+    streams = [splitmix_array(900 + i, (3 << 20) + 77 * i) for i in range(3)]
+    want = {(t, s): as_tuples(oracle.split(tables[t], streams[s], bits=13, min_size=256))
+            for t in range(3) for s in range(3)}
+    assert want[(0, 0)] != want[(1, 0)]                # the tables do change the boundaries
+    order = [(t, s) for s in range(3) for t in (0, 1, 0, 2, 1)]
+    for t, s in order:
+        ch, _ = gpu.split_hash_batch([streams[s]], bits=13, min_size=256, table=tables[t])
+        assert as_tuples(ch) == want[(t, s)], (t, s)
+
+    def run(job):
+        t, s = job
+        ch, _ = gpu.split_hash_batch([streams[s]], bits=13, min_size=256, table=tables[t])
+        return as_tuples(ch) == want[(t, s)]
+    with ThreadPoolExecutor(max_workers=6) as ex:
+        assert all(ex.map(run, order * 2))
