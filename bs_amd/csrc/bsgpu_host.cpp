@@ -2119,6 +2119,7 @@ struct bsg_hasher {
   static constexpr uint32_t kEngineMinBlobs = 16;
   static constexpr uint64_t kEngineMinBytes = 4ull << 20;
   static constexpr uint64_t kEngineBatch = 256ull << 20;  // bytes per engine run (one blob may exceed)
+  static constexpr uint64_t kGatherPiece = 32ull << 20;   // packed and copied to the device at once
   bsg_engine* eng = nullptr;
   PinBuf stage;
   DevBuf dstage;
@@ -2144,9 +2145,21 @@ struct bsg_hasher {
       }
       HCHECK(stage.ensure(bytes + kReadSlack));
       HCHECK(dstage.ensure(bytes + kReadSlack));
-      par_gather(stage.as<uint8_t>(), base, o ? o + i : nullptr, ptrs ? ptrs + i : nullptr, l + i,
-                 aoff.data(), j - i, bytes);
-      if (bytes) HCHECK(hipMemcpyAsync(dstage.p, stage.p, bytes, hipMemcpyHostToDevice, es));
+      // gathered a piece at a time, each piece's H2D queued as soon as it is packed, so the copy
+      // engine moves piece k while the host threads pack piece k+1
+      for (uint32_t a = 0; a < j - i;) {
+        uint32_t b = a;
+        uint64_t pbytes = 0;
+        while (b < j - i && (b == a || pbytes < kGatherPiece)) pbytes += l[i + b++];
+        const uint64_t lo = aoff[a];
+        const uint64_t hi = (b < j - i) ? aoff[b] : bytes;
+        par_gather(stage.as<uint8_t>(), base, o ? o + i + a : nullptr,
+                   ptrs ? ptrs + i + a : nullptr, l + i + a, aoff.data() + a, b - a, pbytes);
+        if (hi > lo)
+          HCHECK(hipMemcpyAsync(dstage.as<uint8_t>() + lo, stage.as<uint8_t>() + lo, hi - lo,
+                                hipMemcpyHostToDevice, es));
+        a = b;
+      }
       int rc = bsg_engine_hash(eng, dstage.as<uint8_t>(), aoff.data(), l + i, j - i);
       uint64_t nch = 0;
       if (!rc) rc = bsg_engine_finish(eng, &nch);
