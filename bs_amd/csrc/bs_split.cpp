@@ -861,6 +861,15 @@ std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err, bool
 
 Reader::~Reader() {
   if (ahead_.valid()) ahead_.wait();  // the background window uses this Reader's store, hasher
+  static const bool debug = std::getenv("BSG_DEBUG_READER") != nullptr;
+  if (debug && verify_)
+    std::fprintf(stderr,
+                 "bsgpu reader: %llu windows on the reading thread (%.1f ms), %llu ahead; "
+                 "%.1f MiB verified: walk %.1f ms, fetch %.1f ms, hash %.1f ms; reads waited "
+                 "%.1f ms for windows ahead\n",
+                 (unsigned long long)tm_.sync_windows, tm_.sync * 1e3,
+                 (unsigned long long)tm_.ahead_windows, tm_.bytes / 1048576.0, tm_.walk * 1e3,
+                 tm_.fetch * 1e3, tm_.hash * 1e3, tm_.wait * 1e3);
 }
 
 // Verify mode. The next leaf node of the walk `cur` (a node with leaves), fetching the internal
@@ -893,6 +902,12 @@ Status Reader::NextLeafNode(std::vector<Frame>* cur, Node* out, bool* done) {
 // long chunks on wave-mode chains). Runs on the reading thread or on the background one.
 Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint64_t budget) {
   Window w;
+  double t = now_s();
+  auto lap = [&t](double* acc) {
+    const double t1 = now_s();
+    *acc += t1 - t;
+    t = t1;
+  };
   std::vector<Node> nodes;
   uint64_t total = 0;
   if (first) {
@@ -912,6 +927,8 @@ Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint
     nodes.push_back(std::move(n));
   }
   w.cursor = std::move(cur);
+  w.bytes = total;
+  lap(&w.t_walk);
   for (const Node& n : nodes) w.covered.push_back(n.offset);
   std::vector<std::vector<Blob>> chunks(nodes.size());
   std::vector<std::pair<size_t, size_t>> all;  // (leaf node, leaf)
@@ -932,6 +949,7 @@ Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint
     }
   };
   bsg::parallel_for(errs.size(), fetch);
+  lap(&w.t_fetch);
   for (const Status& e : errs)
     if (!e.ok()) {
       w.st = e;
@@ -948,6 +966,7 @@ Reader::Window Reader::VerifyRun(std::vector<Frame> cur, const Node* first, uint
     }
   std::vector<Ref> refs(ptrs.size());
   Status s = hasher_->SumPtrs(ptrs.data(), lens.data(), ptrs.size(), refs.data());
+  lap(&w.t_hash);
   if (!s.ok()) {
     w.st = Status::Err(s.code, "verifying chunks: " + s.msg);
     return w;
@@ -973,6 +992,10 @@ Status Reader::TakeLeaf() {
   const bool sequential = at == next_leaf_;
   next_leaf_ = at + stack_.back().size;
   auto take = [&](Window&& w, bool ahead) -> Status {
+    tm_.walk += w.t_walk;
+    tm_.fetch += w.t_fetch;
+    tm_.hash += w.t_hash;
+    tm_.bytes += w.bytes;
     if (!w.st.ok()) {
       window_.clear();
       if (std::find(w.covered.begin(), w.covered.end(), at) != w.covered.end()) return w.st;
@@ -988,7 +1011,11 @@ Status Reader::TakeLeaf() {
   };
   auto it = window_.find(at);
   if (it == window_.end() && sequential && ahead_.valid()) {
-    Status s = take(ahead_.get(), true);
+    const double t0 = now_s();
+    Window w = ahead_.get();
+    tm_.wait += now_s() - t0;
+    tm_.ahead_windows++;
+    Status s = take(std::move(w), true);
     if (!s.ok()) return s;
     it = window_.find(at);
   }
@@ -1008,7 +1035,10 @@ Status Reader::TakeLeaf() {
       while (c < parent.nodes.size() && parent.nodes[c].offset <= on_path) ++c;
       cur.push_back(Frame{parent, c});
     }
+    const double t0 = now_s();
     Window w = VerifyRun(std::move(cur), &stack_.back(), sequential ? window_bytes_ : 0);
+    tm_.sync += now_s() - t0;
+    tm_.sync_windows++;
     if (!w.st.ok()) return w.st;
     Status s = take(std::move(w), sequential);
     if (!s.ok()) return s;

@@ -2122,9 +2122,9 @@ struct bsg_hasher {
   static constexpr uint64_t kGatherPiece = 32ull << 20;   // packed and copied to the device at once
   bsg_engine* eng = nullptr;
   PinBuf stage;
+  PinBuf h_recs;  // an engine run's records, D2H
   DevBuf dstage;
   std::vector<uint64_t> aoff;
-  std::vector<bsg_chunk> recs;
 
   // blob k is base + o[k], or ptrs[k] when ptrs is given (scattered blobs, e.g. a store's)
   int sum_engine(const uint8_t* base, const uint64_t* o, const uint8_t* const* ptrs,
@@ -2132,19 +2132,30 @@ struct bsg_hasher {
     int err = 0;
     if (!eng && !(eng = bsg_engine_create(dev, nullptr, &err))) return err ? err : BSG_EDEVICE;
     hipStream_t es = static_cast<hipStream_t>(bsg_engine_stream(eng));
+    stage.dma_only = true;  // read only by the H2D: a registered huge-page mapping pins faster
+    uint64_t left = 0;      // bytes of the blobs not yet in a run
+    for (uint32_t k = 0; k < n; ++k) left += l[k];
     for (uint32_t i = 0; i < n;) {
+      // A run is up to kEngineBatch bytes, or everything left if that is at most a quarter more:
+      // every run waits for its longest blob's chain (~10 ms for a 256 MiB run), so a small
+      // remainder run (a verifying Reader's window just over 256 MiB) doubled the wait.
+      const uint64_t cap = left <= kEngineBatch + kEngineBatch / 4 ? UINT64_MAX : kEngineBatch;
       uint64_t bytes = 0;
       uint32_t j = i;
       aoff.clear();
       while (j < n && j - i < 65535u) {
         const uint64_t a = (bytes + 15) & ~15ull;
-        if (j > i && a + l[j] > kEngineBatch) break;
+        if (j > i && a + l[j] > cap) break;
         aoff.push_back(a);
         bytes = a + l[j];
+        left -= l[j];
         ++j;
       }
-      HCHECK(stage.ensure(bytes + kReadSlack));
-      HCHECK(dstage.ensure(bytes + kReadSlack));
+      // sized once for the largest run (a growth re-pins: ~35 ms per 256 MiB)
+      const uint64_t want =
+          bytes >= kEngineBatch / 2 ? std::max(bytes, kEngineBatch + kEngineBatch / 4) : bytes;
+      HCHECK(stage.ensure(want + kReadSlack));
+      HCHECK(dstage.ensure(want + kReadSlack));
       // gathered a piece at a time, each piece's H2D queued as soon as it is packed, so the copy
       // engine moves piece k while the host threads pack piece k+1
       for (uint32_t a = 0; a < j - i;) {
@@ -2165,9 +2176,14 @@ struct bsg_hasher {
       if (!rc) rc = bsg_engine_finish(eng, &nch);
       if (!rc && nch != j - i) rc = BSG_EDEVICE;
       if (rc) return rc;
-      recs.resize(j - i);
-      if ((rc = bsg_engine_copy_chunks(eng, recs.data(), j - i))) return rc;
-      for (uint32_t k = 0; k < j - i; ++k) std::memcpy(out + 32ull * (i + k), recs[k].ref, 32);
+      // the records through pinned memory (a D2H into a fresh pageable vector cost ~12 ms the
+      // first time: the runtime pins its pages)
+      HCHECK(h_recs.ensure(sizeof(bsg_chunk) * (j - i)));
+      HCHECK(hipMemcpyAsync(h_recs.p, eng->out.p, sizeof(bsg_chunk) * (j - i),
+                            hipMemcpyDeviceToHost, es));
+      HCHECK(hipStreamSynchronize(es));
+      const bsg_chunk* rec = h_recs.as<bsg_chunk>();
+      for (uint32_t k = 0; k < j - i; ++k) std::memcpy(out + 32ull * (i + k), rec[k].ref, 32);
       i = j;
     }
     return BSG_OK;
@@ -2284,6 +2300,7 @@ void bsg_hasher_free(bsg_hasher* h) {
   h->h_meta.release();
   h->h_small.release();
   h->stage.release();
+  h->h_recs.release();
   h->dstage.release();
   if (h->eng) bsg_engine_destroy(h->eng);
   if (h->stream) stream_release(h->dev, h->stream, h->prio);

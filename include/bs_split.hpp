@@ -353,6 +353,8 @@ class Reader {
     std::vector<uint64_t> covered;  // its leaf-node offsets (also when verification failed)
     Status st;
     bool end = false;               // the walk reached the last leaf node
+    double t_walk = 0, t_fetch = 0, t_hash = 0;  // seconds in VerifyRun's phases
+    uint64_t bytes = 0;
   };
   Status NextLeafNode(std::vector<Frame>* cur, Node* out, bool* done);
   Window VerifyRun(std::vector<Frame> cur, const Node* first, uint64_t budget);
@@ -370,6 +372,13 @@ class Reader {
   std::unique_ptr<GpuHasher> hasher_;
   // the next window, fetched and verified on a background thread while this one is read
   std::future<Window> ahead_;
+  // where a verifying Reader's time goes (seconds), printed when it is destroyed if
+  // BSG_DEBUG_READER is set: windows verified on the reading thread / ahead, VerifyRun's phases
+  // summed over all windows, and what reads waited for the window verified ahead
+  struct Timing {
+    double walk = 0, fetch = 0, hash = 0, wait = 0, sync = 0;
+    uint64_t sync_windows = 0, ahead_windows = 0, bytes = 0;
+  } tm_;
 
  public:
   ~Reader();
