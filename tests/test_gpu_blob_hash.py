@@ -46,6 +46,33 @@ def test_hasher_sum_ptrs_engine_and_small(gpu):
         h.free()
 
 
+@pytest.fixture(scope="module")
+def shared_hasher(gpu):
+    h = gpu.Hasher()
+    yield h
+    h.free()
+
+
+@pytest.mark.parametrize("total_mib,big_mib", [(262, 0), (700, 0), (180, 330)])
+def test_hasher_runs_around_256mib(gpu, shared_hasher, total_mib, big_mib):
+    """The engine path splits a host batch into runs of 256 MiB, but takes everything left in
+    one run when it is at most a quarter more (a Reader window just over 256 MiB), and a blob
+    longer than a run alone; the staging is sized once for the largest run. 262 MiB: one run;
+    700 MiB: 256 + 444 -> 256 + 256 + 188; a 330 MiB blob among 180 MiB of others. Every ref
+    equals hashlib's, on one persistent hasher reused across the three shapes."""
+    rng = np.random.default_rng(total_mib)
+    n = (total_mib << 20) // 65_000
+    lens = rng.integers(1_000, 129_000, n)
+    data = np.frombuffer(rng.bytes(int(lens.sum()) + (big_mib << 20)), dtype=np.uint8)
+    blobs, o = [], 0
+    for ln in lens:
+        blobs.append(data[o:o + int(ln)].tobytes())
+        o += int(ln)
+    if big_mib:
+        blobs.insert(len(blobs) // 2, data[o:o + (big_mib << 20)].tobytes())
+    assert shared_hasher.sum_ptrs(blobs) == [hashlib.sha256(b).digest() for b in blobs]
+
+
 def test_sha256_batch_over_65535_blobs(gpu):
     rng = np.random.default_rng(8)
     lens = rng.integers(0, 160, 70_000)
