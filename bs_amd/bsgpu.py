@@ -9,6 +9,7 @@ Fanout (/root/reference/split/split.go:44-165) and bs.Blob.Ref (/root/reference/
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import re
@@ -109,6 +110,7 @@ def lib() -> ctypes.CDLL:
         "bsg_hasher_sum_ptrs": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_void_p), u64p,
                                                ctypes.c_uint32, vp]),
         "bsg_hasher_free": (None, [vp]),
+        "bsg_hasher_pinned_bytes": (ctypes.c_size_t, [vp]),
         "bsg_fill_splitmix": (ctypes.c_int, [ctypes.c_int, vp, ctypes.c_uint64, ctypes.c_uint64,
                                              vp]),
         "bsg_device_malloc": (vp, [ctypes.c_int, ctypes.c_size_t]),
@@ -143,6 +145,11 @@ def lib() -> ctypes.CDLL:
         "bsg_reader_read": (ctypes.c_int64, [vp, vp, ctypes.c_size_t]),
         "bsg_reader_seek": (ctypes.c_int64, [vp, ctypes.c_int64, ctypes.c_int]),
         "bsg_reader_size": (ctypes.c_uint64, [vp]),
+        "bsg_reader_stats": (ctypes.c_int, [vp, u64p]),
+        "bsg_debug_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64]),
+        "bsg_debug_get": (ctypes.c_int64, [ctypes.c_int]),
+        "bsg_set_stream_base": (ctypes.c_int, [vp, ctypes.c_uint64]),
+        "bsg_writer_set_stream_base": (ctypes.c_int, [vp, ctypes.c_uint64]),
         "bsg_reader_free": (None, [vp]),
     }
     partial = os.environ.get("BSG_LIB_PARTIAL") == "1"  # A/B of older builds (tools/)
@@ -174,6 +181,28 @@ def _u64(a) -> np.ndarray:
 
 def _p(a: np.ndarray, ct):
     return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW = 1, 2, 3  # bsg_debug_set knobs
+
+
+def debug_get(knob: int) -> int:
+    return int(lib().bsg_debug_get(knob))
+
+
+def debug_set(knob: int, value: int) -> None:
+    """bsg_debug_set: a process-wide test knob (no environment changes at run time)."""
+    _check(lib().bsg_debug_set(knob, value), "bsg_debug_set")
+
+
+@contextlib.contextmanager
+def debug_knob(knob: int, value: int):
+    old = debug_get(knob)
+    debug_set(knob, value)
+    try:
+        yield
+    finally:
+        debug_set(knob, old)
 
 
 def device_count() -> int:
@@ -260,6 +289,22 @@ class Hasher:
         _check(lib().bsg_hasher_sum_ptrs(self.h, ptrs, _p(lens, ctypes.c_uint64), len(blobs),
                                          refs.ctypes.data), "bsg_hasher_sum_ptrs")
         return [refs[32 * i:32 * i + 32].tobytes() for i in range(len(blobs))]
+
+    def sum(self, blobs: list) -> list[bytes]:
+        """Blobs packed into one host buffer (bsg_hasher_sum)."""
+        arrs = [np.frombuffer(bytes(b), dtype=np.uint8) for b in blobs]
+        lens = _u64([len(a) for a in arrs])
+        off = _u64(np.concatenate([[0], np.cumsum(lens)[:-1]]) if arrs else [])
+        base = np.concatenate(arrs) if arrs and sum(len(a) for a in arrs) else np.zeros(1, np.uint8)
+        refs = np.zeros(32 * max(len(arrs), 1), dtype=np.uint8)
+        _check(lib().bsg_hasher_sum(self.h, base.ctypes.data, _p(off, ctypes.c_uint64),
+                                    _p(lens, ctypes.c_uint64), len(arrs), refs.ctypes.data),
+               "bsg_hasher_sum")
+        return [refs[32 * i:32 * i + 32].tobytes() for i in range(len(blobs))]
+
+    def pinned_bytes(self) -> int:
+        """bsg_hasher_pinned_bytes: pinned host memory the hasher holds (diagnostics)."""
+        return int(lib().bsg_hasher_pinned_bytes(self.h))
 
     def free(self):
         if self.h:
@@ -434,6 +479,10 @@ class StreamingSplitter:
             _check(lib().bsg_set_tile(self.h, tile), "bsg_set_tile")
         if carry_cap is not None:
             _check(lib().bsg_set_carry_cap(self.h, carry_cap), "bsg_set_carry_cap")
+
+    def set_stream_base(self, base: int) -> None:
+        """bsg_set_stream_base (tests): the stream's first byte has offset `base`."""
+        _check(lib().bsg_set_stream_base(self.h, base), "bsg_set_stream_base")
 
     def write(self, data) -> int:
         a = _as_u8(data)
@@ -638,6 +687,10 @@ class Writer:
             raise BsgError(err.value, "bsg_writer_new")
         self.store = store
 
+    def set_stream_base(self, base: int) -> None:
+        """bsg_writer_set_stream_base (tests), before the first write."""
+        _check(lib().bsg_writer_set_stream_base(self.h, base), "bsg_writer_set_stream_base")
+
     def write(self, data) -> int:
         a = _as_u8(data)
         _check(lib().bsg_writer_write(self.h, a.ctypes.data, a.nbytes), "Write")
@@ -697,6 +750,14 @@ class Reader:
     @property
     def size(self) -> int:
         return lib().bsg_reader_size(self.h)
+
+    def stats(self) -> dict:
+        """bsg_reader_stats (verify mode): windows verified on the reading thread / taken from
+        the read-ahead, bytes verified, read-ahead windows dropped after a seek."""
+        out = np.zeros(4, dtype=np.uint64)
+        _check(lib().bsg_reader_stats(self.h, _p(out, ctypes.c_uint64)), "bsg_reader_stats")
+        return {"sync_windows": int(out[0]), "ahead_windows": int(out[1]),
+                "bytes": int(out[2]), "dropped": int(out[3])}
 
     def free(self):
         if self.h:

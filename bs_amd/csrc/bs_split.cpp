@@ -562,6 +562,14 @@ Status Writer::Add(const Ref& ref, uint64_t len, unsigned level) {  // TreeBuild
   return Status::Ok();
 }
 
+Status Writer::SetStreamBase(uint64_t base) {
+  if (end_ != base_ || closed_) return Status::Err(BSG_ESTATE, "stream base after the first Write");
+  const int rc = bsg_set_stream_base(ctx_, base);
+  if (rc) return Status::Err(rc, std::string("bsg_set_stream_base: ") + bsg_errstr(rc));
+  base_ = end_ = emitted_ = base;
+  return Status::Ok();
+}
+
 size_t Writer::TakeRecords(std::vector<bsg_chunk>* out) {
   out->clear();
   const size_t n = bsg_pending(ctx_);
@@ -852,8 +860,8 @@ std::unique_ptr<Reader> Reader::New(Store* g, const Ref& root, Status* err, bool
   r->g_ = g;
   r->verify_ = verify;
   r->device_ = device;
-  if (const char* e = std::getenv("BSG_VERIFY_WINDOW"))  // tests: small windows
-    r->window_bytes_ = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  if (const int64_t wb = bsg_debug_get(BSG_KNOB_VERIFY_WINDOW))  // tests: small windows
+    r->window_bytes_ = (uint64_t)wb;
   r->stack_.push_back(std::move(n));
   *err = Status::Ok();
   return r;
@@ -991,6 +999,10 @@ Status Reader::TakeLeaf() {
   // random or backward read costs one leaf node's fetch and hash, not a 256 MiB window.
   const bool sequential = at == next_leaf_;
   next_leaf_ = at + stack_.back().size;
+  // A window in flight when the reader seeks was started for the old position: it is never
+  // taken (taking it would start yet another full window from the old cursor), only waited for
+  // and dropped when the next window ahead is started.
+  if (!sequential && ahead_.valid()) ahead_stale_ = true;
   auto take = [&](Window&& w, bool ahead) -> Status {
     tm_.walk += w.t_walk;
     tm_.fetch += w.t_fetch;
@@ -1002,15 +1014,21 @@ Status Reader::TakeLeaf() {
       return Status::Ok();  // a failure further on, in a window this read does not need
     }
     window_ = std::move(w.leaves);
-    if (!w.end && ahead)
+    if (!w.end && ahead) {
+      if (ahead_.valid()) {  // a stale window (see above): dropped here
+        ahead_.wait();
+        tm_.dropped++;
+      }
+      ahead_stale_ = false;
       ahead_ = std::async(std::launch::async,
                           [this, cur = std::move(w.cursor)]() mutable {
                             return VerifyRun(std::move(cur), nullptr, window_bytes_);
                           });
+    }
     return Status::Ok();
   };
   auto it = window_.find(at);
-  if (it == window_.end() && sequential && ahead_.valid()) {
+  if (it == window_.end() && sequential && ahead_.valid() && !ahead_stale_) {
     const double t0 = now_s();
     Window w = ahead_.get();
     tm_.wait += now_s() - t0;
@@ -1021,8 +1039,12 @@ Status Reader::TakeLeaf() {
   }
   if (it == window_.end()) {
     if (sequential) {  // a window read ahead for elsewhere in the stream: dropped
-      if (ahead_.valid()) ahead_.wait();
+      if (ahead_.valid()) {
+        ahead_.wait();
+        tm_.dropped++;
+      }
       ahead_ = std::future<Window>();
+      ahead_stale_ = false;
     }
     if (!hasher_) hasher_.reset(new GpuHasher(device_));
     // the walk, positioned after stack_.back(): each internal node on the path and its child
@@ -1307,6 +1329,9 @@ int bsg_writer_write(bsg_writer* w, const uint8_t* p, size_t n) {
   return w->w->Write(p, n).code;
 }
 int bsg_writer_close(bsg_writer* w) { return w ? w->w->Close().code : BSG_EINVAL; }
+int bsg_writer_set_stream_base(bsg_writer* w, uint64_t base) {
+  return w ? w->w->SetStreamBase(base).code : BSG_EINVAL;
+}
 int bsg_writer_root(const bsg_writer* w, uint8_t out[32]) {
   if (!w || !out) return BSG_EINVAL;
   std::memcpy(out, w->w->Root().data(), 32);
@@ -1350,6 +1375,11 @@ int64_t bsg_reader_seek(bsg_reader* r, int64_t off, int whence) {
   return r ? (int64_t)r->r->Seek(off, whence) : BSG_EINVAL;
 }
 uint64_t bsg_reader_size(const bsg_reader* r) { return r ? r->r->Size() : 0; }
+int bsg_reader_stats(const bsg_reader* r, uint64_t out[4]) {
+  if (!r || !out) return BSG_EINVAL;
+  r->r->Stats(out);
+  return BSG_OK;
+}
 void bsg_reader_free(bsg_reader* r) { delete r; }
 
 }  // extern "C"

@@ -248,21 +248,37 @@ hipError_t dbg(const char* what, hipStream_t s, hipError_t e) {
   return e;
 }
 
-// Polls of a k_sha helper-wave handshake before it gives up and flags a device error (~1 s).
-// BSG_DEBUG_SEQ_WAIT=<n> overrides it (read at every run): 0 makes every handshake fail at once,
-// which is how the tests drive the device-error path (Counters::error -> BSG_EDEVICE).
-uint32_t seq_wait_limit() {
-  const char* e = std::getenv("BSG_DEBUG_SEQ_WAIT");
-  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (1u << 24);
+// Test and debug knobs (bsg_debug_set). Each starts from its environment variable, read once
+// (a getenv racing a test's setenv on another thread is a data race in glibc), and tests change
+// it through bsg_debug_set instead of the environment.
+std::atomic<int64_t>& knob(int k) {
+  static std::atomic<int64_t> seq_wait{[] {
+    // polls of a k_sha helper-wave handshake before it gives up and flags a device error
+    // (~1 s); 0 makes every handshake fail at once, which is how the tests drive the
+    // device-error path (Counters::error -> BSG_EDEVICE)
+    const char* e = std::getenv("BSG_DEBUG_SEQ_WAIT");
+    return e ? (int64_t)std::strtoul(e, nullptr, 10) : (int64_t)(1u << 24);
+  }()};
+  static std::atomic<int64_t> long_mode{[] {  // BSG_LONG_MODE = off | all (experiments)
+    const char* e = std::getenv("BSG_LONG_MODE");
+    if (e && !std::strcmp(e, "off")) return (int64_t)1;
+    if (e && !std::strcmp(e, "all")) return (int64_t)2;
+    return (int64_t)0;
+  }()};
+  static std::atomic<int64_t> verify_window{[] {  // split::Reader window (0: 256 MiB)
+    const char* e = std::getenv("BSG_VERIFY_WINDOW");
+    return e ? (int64_t)std::strtoull(e, nullptr, 10) : (int64_t)0;
+  }()};
+  static std::atomic<int64_t> none{0};
+  switch (k) {
+    case BSG_KNOB_SEQ_WAIT: return seq_wait;
+    case BSG_KNOB_LONG_MODE: return long_mode;
+    case BSG_KNOB_VERIFY_WINDOW: return verify_window;
+    default: return none;
+  }
 }
-
-int long_mode() {  // BSG_LONG_MODE = off | all (experiments); default auto
-  const char* e = std::getenv("BSG_LONG_MODE");
-  if (!e) return 0;
-  if (!std::strcmp(e, "off")) return 1;
-  if (!std::strcmp(e, "all")) return 2;
-  return 0;
-}
+uint32_t seq_wait_limit() { return (uint32_t)knob(BSG_KNOB_SEQ_WAIT).load(); }
+int long_mode() { return (int)knob(BSG_KNOB_LONG_MODE).load(); }
 
 #define HCHECK(x)                           \
   do {                                      \
@@ -453,7 +469,7 @@ struct bsg_engine {
 
     ChunkArgs ca{cand.as<uint64_t>(), flags.as<uint32_t>(), fidx.as<uint64_t>(),
                  bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
-                 last_end.as<uint64_t>(), chunk_cap, p, dctr};
+                 last_end.as<uint64_t>(), chunk_cap, p, dctr, streams.as<StreamDesc>()};
     HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, ns, stream, num_cus)));
     if (snapshot) {  // by kernel, not by the copy engine (see launch_copy_out)
       HCHECK(h_snap.ensure(sizeof(Counters) + 8ull * (ns ? ns : 1)));
@@ -522,7 +538,8 @@ struct bsg_engine {
     mark(0);
     mark(1);  // no scan / selection stage
     ChunkArgs ca{nullptr, nullptr, nullptr, bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(),
-                 scount.as<uint64_t>(), last_end.as<uint64_t>(), chunk_cap, p, dctr};
+                 scount.as<uint64_t>(), last_end.as<uint64_t>(), chunk_cap, p, dctr,
+                 streams.as<StreamDesc>()};
     if (ns) HCHECK(dbg("launch_blob_jobs", stream,
                        launch_blob_jobs(ca, streams.as<StreamDesc>(), ns, stream, num_cus)));
     ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
@@ -914,6 +931,7 @@ struct bsg_ctx {
   int prev = -1;            // last submitted slot (its open chunk continues into `cur`)
   std::deque<int> inflight; // submitted slots in stream order
   uint64_t pos = 0;         // stream offset of slots[cur]'s first byte
+  uint64_t stream0 = 0;     // stream offset of the stream's first byte (0; bsg_set_stream_base)
   uint8_t hist[64];         // the 64 stream bytes before pos
   uint8_t tail[64];         // the last 64 stream bytes copied to the device so far
   std::deque<bsg_chunk> ready;
@@ -1153,6 +1171,7 @@ struct bsg_ctx {
     d.data_off = carry_cap;
     d.len = fill;
     d.seg_base = pos;
+    d.open_start = stream0;  // the first tile; later tiles take the previous tile's open chunk
     d.finalize = final_seg ? 1u : 0u;
     d.carry_cap = final_seg ? 0u : (uint32_t)std::min<uint64_t>(carry_cap, 0xffffffffu);
     std::memcpy(d.hist, hist, 64);
@@ -1222,13 +1241,10 @@ struct bsg_ctx {
   }
 
   // Host side of Write: bytes into the staging ring (large pieces on several threads), each full
-  // stage on its way to the device at once, full tiles submitted as more data arrives.
-  // Stream offsets travel in 40-bit candidate fields (bsgpu_internal.h): 1 TiB per stream.
-  static constexpr uint64_t kMaxStream = 1ull << 40;
-  bool too_long(size_t n) const { return pos + fill + n >= kMaxStream; }
-
+  // stage on its way to the device at once, full tiles submitted as more data arrives. A stream
+  // has no length limit (split.Writer.Write has none, split/split.go:99-101): stream offsets are
+  // u64 everywhere; only candidate positions inside one tile travel in 40-bit fields.
   int write(const uint8_t* p, size_t n) {
-    if (too_long(n)) return BSG_EINVAL;
     while (n) {
       if (fill == tile) {  // full tile and more data coming: submit it (never the last one)
         int rc = submit(false);
@@ -1265,7 +1281,6 @@ struct bsg_ctx {
   // full tile always keeps unflushed bytes that window() can hold back for the next tile (a
   // final segment needs at least one byte).
   int write_pinned(const uint8_t* q, size_t n) {
-    if (too_long(n)) return BSG_EINVAL;
     while (n) {
       if (fill == tile) {
         int rc = submit(false);
@@ -1326,7 +1341,7 @@ struct bsg_ctx {
     return BSG_OK;
   }
   int commit(size_t n) {
-    if (n > std::min(stage_room(), tile - fill) || too_long(n)) return BSG_EINVAL;
+    if (n > std::min(stage_room(), tile - fill)) return BSG_EINVAL;
     sfill += n;
     fill += n;
     if (stage_room() == 0 && fill < tile) {
@@ -1377,6 +1392,7 @@ struct bsg_ctx {
     scur = 0;
     sfill = 0;
     prev = -1;
+    stream0 = 0;
     pos = 0;
     std::memset(hist, 0, 64);
     std::memset(tail, 0, 64);
@@ -1387,7 +1403,7 @@ struct bsg_ctx {
   }
 
   int close_begin() {
-    if (fill == 0 && pos == 0) return BSG_OK;  // empty stream: no chunks
+    if (fill == 0 && pos == stream0) return BSG_OK;  // empty stream: no chunks
     // The final segment must hold at least one byte: the open chunk's flush is emitted by the
     // scan of its last strip. write() and window() never submit a tile without leaving bytes
     // behind, so this cannot happen; fail loudly rather than drop the last chunk.
@@ -1411,6 +1427,18 @@ struct bsg_ctx {
 // C ABI
 // ------------------------------------------------------------------------------------------
 extern "C" {
+
+int64_t bsg_debug_get(int k) {
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_VERIFY_WINDOW) return -1;
+  return knob(k).load();
+}
+
+int bsg_debug_set(int k, int64_t value) {
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_VERIFY_WINDOW || value < 0) return BSG_EINVAL;
+  if (k == BSG_KNOB_LONG_MODE && value > 2) return BSG_EINVAL;
+  knob(k).store(value);
+  return BSG_OK;
+}
 
 const char* bsg_errstr(int err) {
   switch (err) {
@@ -1756,14 +1784,21 @@ bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, i
 }
 
 int bsg_set_tile(bsg_ctx* c, size_t tile) {
-  if (!c || tile < 4096 || c->fill || c->pos || c->started) return BSG_EINVAL;
+  if (!c || tile < 4096 || c->fill || c->pos != c->stream0 || c->started) return BSG_EINVAL;
   c->tile = tile;
   return BSG_OK;
 }
 
 int bsg_set_carry_cap(bsg_ctx* c, size_t bytes) {
-  if (!c || c->fill || c->pos || c->started || bytes > 0xffffffffull) return BSG_EINVAL;
+  if (!c || c->fill || c->pos != c->stream0 || c->started || bytes > 0xffffffffull)
+    return BSG_EINVAL;
   c->carry_cap = bytes;
+  return BSG_OK;
+}
+
+int bsg_set_stream_base(bsg_ctx* c, uint64_t base) {
+  if (!c || c->fill || c->pos != c->stream0 || c->started || c->closed) return BSG_EINVAL;
+  c->stream0 = c->pos = base;
   return BSG_OK;
 }
 
@@ -2211,12 +2246,19 @@ struct bsg_hasher {
     HCHECK(h_meta.ensure(16ull * n));
     std::memcpy(h_meta.p, o, 8ull * n);
     std::memcpy(h_meta.as<uint8_t>() + 8ull * n, l, 8ull * n);
-    // host bytes (tree nodes: pageable std::string) go through pinned memory, whose H2D / D2H
-    // are single DMAs instead of the runtime's chunked staging of pageable memory
-    HCHECK(h_small.ensure(std::max<uint64_t>(on_device ? 0 : hi, 32ull * n)));
+    // Small host batches (tree nodes: pageable std::string) go through pinned memory, whose
+    // H2D / D2H are single DMAs instead of the runtime's chunked staging of pageable memory.
+    // The path is chosen by blob count, so one large blob can land here too: above
+    // kEngineMinBytes its bytes are copied straight from pageable memory instead, so that a
+    // pooled hasher never keeps a blob-sized pinned buffer (pinning costs ~50-65 ms per 256 MiB
+    // and would stay held for the life of the process).
+    const bool via_pinned = !on_device && hi <= kEngineMinBytes;
+    HCHECK(h_small.ensure(std::max<uint64_t>(via_pinned ? hi : 0, 32ull * n)));
     if (hi) {
       if (on_device) {
         HCHECK(hipMemcpyAsync(data.p, base, hi, hipMemcpyDeviceToDevice, stream));
+      } else if (!via_pinned) {
+        HCHECK(hipMemcpyAsync(data.p, base, hi, hipMemcpyHostToDevice, stream));
       } else {
         std::memcpy(h_small.p, base, hi);
         HCHECK(hipMemcpyAsync(data.p, h_small.p, hi, hipMemcpyHostToDevice, stream));
@@ -2287,6 +2329,11 @@ int bsg_hasher_sum_ptrs(bsg_hasher* h, const uint8_t* const* ptrs, const uint64_
     o += len[i];
   }
   return h->sum(packed.data(), off.data(), len, n, refs);
+}
+
+size_t bsg_hasher_pinned_bytes(const bsg_hasher* h) {
+  if (!h) return 0;
+  return h->h_meta.cap + h->h_small.cap + h->stage.cap + h->h_recs.cap;
 }
 
 void bsg_hasher_free(bsg_hasher* h) {

@@ -129,7 +129,6 @@ struct StripCtx {
   uint64_t start;      // segment offset of the strip
   uint32_t count;      // candidates found so far
   uint64_t wbase;      // WRITE mode: first output index
-  uint64_t seg_base;
 };
 
 template <bool WRITE>
@@ -137,7 +136,7 @@ __device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t st
                                      uint64_t seg_off, bool force, uint32_t tz) {
   if (WRITE) {
     uint64_t idx = c.wbase + c.count;
-    if (idx < a.cand_cap) a.cand[idx] = cand_pack(c.stream, c.seg_base + seg_off, force, tz);
+    if (idx < a.cand_cap) a.cand[idx] = cand_pack(c.stream, seg_off, force, tz);
   } else {
     if (c.count < (uint32_t)kSlotCap)
       a.slots[strip * kSlotCap + c.count] = slot_pack((uint32_t)(seg_off - c.start), force, tz);
@@ -431,7 +430,6 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
   c.start = l.start;
   c.count = 0;
   c.wbase = wbase;
-  c.seg_base = sd->seg_base;
   while (hits) {
     const uint64_t off = l.start + 64ull * (uint32_t)__builtin_ctz(hits);
     hits &= hits - 1;
@@ -529,7 +527,7 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a) {
       st = find_stream(a.strip0, a.nstreams, strip);
       first = a.strip0[st];
     }
-    const uint64_t start = a.streams[st].seg_base + (strip - first) * (uint64_t)kStrip;
+    const uint64_t start = (strip - first) * (uint64_t)kStrip;  // segment-relative
     for (uint32_t i = 0; i < cnt; ++i) {
       const uint32_t v = a.slots[strip * kSlotCap + i];
       if (base + i < a.cand_cap)
@@ -669,29 +667,36 @@ __global__ __launch_bounds__(256) void k_select(SelArgs a) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const uint64_t c = a.cand[i];
     const uint32_t s = cand_stream(c);
-    const uint64_t E = cand_pos(c) + 1;  // end (exclusive) if this candidate is a boundary
+    // Candidate positions are segment-relative (40 bits: a segment is < 2^40 bytes of device
+    // memory); the open chunk's start and the boundaries are absolute stream offsets (u64), so
+    // a stream may run past 2^40 bytes, as split.Writer.Write allows (split/split.go:99-101).
+    const uint64_t Er = cand_pos(c) + 1;  // segment-relative end if this candidate is a boundary
     const bool first = (i == 0) || cand_stream(a.cand[i - 1]) != s;
+    if (!first) {
+      const uint64_t pEr = cand_pos(a.cand[i - 1]) + 1;
+      if (Er - pEr < minsz) continue;  // not a sync point: covered by an earlier walk
+    }
+    const uint64_t sb = a.streams[s].seg_base;
     uint64_t last, j;
     if (first) {
       last = a.streams[s].open_start;
       j = i;
     } else {
-      const uint64_t pE = cand_pos(a.cand[i - 1]) + 1;
-      if (E - pE < minsz) continue;  // not a sync point: covered by an earlier walk
       a.flags[i] = 1;
-      last = E;
+      last = sb + Er;
       j = i + 1;
     }
-    uint64_t prevE = first ? 0 : E;
+    uint64_t prevEr = first ? 0 : Er;
     for (; j < total; ++j) {
       const uint64_t cj = a.cand[j];
       if (cand_stream(cj) != s) break;
-      const uint64_t Ej = cand_pos(cj) + 1;
-      if (j > i && Ej - prevE >= minsz) break;  // next sync point starts its own walk
+      const uint64_t Ejr = cand_pos(cj) + 1;
+      if (j > i && Ejr - prevEr >= minsz) break;  // next sync point starts its own walk
+      const uint64_t Ej = sb + Ejr;
       const bool f = cand_force(cj) ? (Ej > last) : (Ej - last >= minsz);
       a.flags[j] = f ? 1u : 0u;
       if (f) last = Ej;
-      prevE = Ej;
+      prevEr = Ejr;
     }
   }
 }
@@ -708,7 +713,7 @@ __global__ __launch_bounds__(256) void k_chunks(ChunkArgs a) {
     const uint32_t s = cand_stream(c);
     const uint32_t tz = cand_tz(c);
     const uint32_t level = tz >= bits ? tz - bits : 0u;
-    const uint64_t E = cand_pos(c) + 1;
+    const uint64_t E = a.streams[s].seg_base + cand_pos(c) + 1;  // absolute stream offset
     if (k >= a.chunk_cap) {  // cannot happen if selection is right (chunks >= MinSize)
       atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 1ull);
       continue;

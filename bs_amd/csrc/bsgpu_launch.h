@@ -56,6 +56,7 @@ struct ChunkArgs {
   uint64_t chunk_cap;
   Params p;
   Counters* ctr;
+  const StreamDesc* streams;  // k_chunks: seg_base turns relative candidates into offsets
 };
 
 struct InitArgs {

@@ -257,6 +257,10 @@ class Writer {
   // Flushes the final chunk, builds the tree root; Root() is valid afterwards. Idempotent.
   Status Close();
   const Ref& Root() const { return root_; }
+  // Tests: the stream's first byte has stream offset `base` on the device (bsg_set_stream_base),
+  // so that offsets past 2^40 are exercised without writing 1 TiB. Before the first Write; the
+  // tree (offsets from 0, as split.Writer's) is unchanged.
+  Status SetStreamBase(uint64_t base);
 
   struct TBNode;
   struct Wrapped;
@@ -335,6 +339,14 @@ class Reader {
   // io.Seeker (whence: 0 start, 1 current, 2 end).
   uint64_t Seek(int64_t offset, int whence);
   uint64_t Size() const { return stack_.front().size; }
+  // Verify mode diagnostics: [0] windows verified on the reading thread, [1] windows taken from
+  // the background read-ahead, [2] bytes verified, [3] windows started ahead and dropped.
+  void Stats(uint64_t out[4]) const {
+    out[0] = tm_.sync_windows;
+    out[1] = tm_.ahead_windows;
+    out[2] = tm_.bytes;
+    out[3] = tm_.dropped;
+  }
 
  private:
   Reader() = default;
@@ -372,12 +384,13 @@ class Reader {
   std::unique_ptr<GpuHasher> hasher_;
   // the next window, fetched and verified on a background thread while this one is read
   std::future<Window> ahead_;
+  bool ahead_stale_ = false;  // ahead_ was started before a seek: never taken, only dropped
   // where a verifying Reader's time goes (seconds), printed when it is destroyed if
   // BSG_DEBUG_READER is set: windows verified on the reading thread / ahead, VerifyRun's phases
   // summed over all windows, and what reads waited for the window verified ahead
   struct Timing {
     double walk = 0, fetch = 0, hash = 0, wait = 0, sync = 0;
-    uint64_t sync_windows = 0, ahead_windows = 0, bytes = 0;
+    uint64_t sync_windows = 0, ahead_windows = 0, bytes = 0, dropped = 0;
   } tm_;
 
  public:

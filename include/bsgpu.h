@@ -84,8 +84,9 @@ typedef struct bsg_ctx bsg_ctx;
 bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table /* 256 or NULL */,
                   int* err);
 /* Copies p[0..n) into pinned staging (the caller keeps ownership of p); full tiles are split
- * and hashed on the device as they fill. A stream may hold up to 2^40 - 1 bytes (1 TiB; stream
- * offsets travel in 40-bit fields on the device): a Write past that returns BSG_EINVAL. */
+ * and hashed on the device as they fill. A stream has no length limit, as split.Writer.Write
+ * (split/split.go:99-101): stream offsets are 64-bit throughout; only positions inside one
+ * device tile (< 2^40 bytes of device memory) travel in 40-bit fields. */
 int bsg_write(bsg_ctx* ctx, const uint8_t* p, size_t n);
 /* Zero-copy Write: *p / *cap = the free rest of the current pinned staging buffer (at most
  * 64 MiB and never more than the rest of the tile; a stream's first buffer grows from 4 MiB,
@@ -124,6 +125,10 @@ int bsg_set_tile(bsg_ctx* ctx, size_t tile_bytes);
  * one is carried as a SHA-256 midstate, which makes the next tile wait for this tile's hashes.
  * 0 = always midstate (tests). Call before the first write. */
 int bsg_set_carry_cap(bsg_ctx* ctx, size_t bytes);
+/* Tests: the stream's first byte has stream offset `base` (records carry offsets from it, the
+ * split is unchanged), so that offsets past 2^40 can be exercised without writing 1 TiB. Call
+ * before the first write; bsg_reset goes back to 0. */
+int bsg_set_stream_base(bsg_ctx* ctx, uint64_t base);
 /* Start a new stream on the same context (its device and pinned buffers are kept), as a
  * pool of split.Writers would; undrained chunks of the previous stream are discarded. */
 int bsg_reset(bsg_ctx* ctx);
@@ -134,7 +139,8 @@ typedef struct bsg_engine bsg_engine;
 bsg_engine* bsg_engine_create(int device, const uint32_t* table /* 256 or NULL */, int* err);
 void bsg_engine_destroy(bsg_engine* eng);
 /* Enqueue split + hash of nstreams streams d_data[off[i] .. off[i]+len[i]) (device memory,
- * off[i] % 16 == 0; off/len are host arrays; at most 65,535 streams of < 2^40 bytes each).
+ * off[i] % 16 == 0; off/len are host arrays; at most 65,535 streams of < 2^40 bytes each, a
+ * device-memory bound: one stream of a run lies whole in device memory).
  * Asynchronous on the engine's stream.
  * The allocation holding d_data must extend at least BSG_READ_SLACK bytes past the end of the
  * last stream (the SHA-256 loader reads whole 64-byte blocks and masks the excess). */
@@ -201,6 +207,10 @@ int bsg_hasher_sum(bsg_hasher* h, const uint8_t* base, const uint64_t* off, cons
 int bsg_hasher_sum_ptrs(bsg_hasher* h, const uint8_t* const* ptrs, const uint64_t* len,
                         uint32_t n, uint8_t* refs);
 void bsg_hasher_free(bsg_hasher* h);
+/* Diagnostics: bytes of pinned host memory the hasher holds (its small-batch buffer, its
+ * metadata and record buffers, its large-batch staging). A large blob hashed through the
+ * small-batch path is copied from pageable memory and does not grow it. */
+size_t bsg_hasher_pinned_bytes(const bsg_hasher* h);
 
 /* Device memory helpers (so callers need no second HIP runtime): kind 0 = H2D, 1 = D2H,
  * 2 = D2D. */
@@ -254,6 +264,9 @@ bsg_writer* bsg_writer_new(int device, bsg_store* s, const bsg_params* params, s
                            int* err);
 int bsg_writer_write(bsg_writer* w, const uint8_t* p, size_t n);
 int bsg_writer_close(bsg_writer* w);
+/* Tests: bsg_set_stream_base for the Writer's context, before the first bsg_writer_write; the
+ * Writer's tree and Root are unchanged (tree offsets start at 0, as split.Writer's). */
+int bsg_writer_set_stream_base(bsg_writer* w, uint64_t base);
 int bsg_writer_root(const bsg_writer* w, uint8_t out[32]);
 void bsg_writer_free(bsg_writer* w);
 
@@ -269,7 +282,20 @@ bsg_reader* bsg_reader_open(bsg_store* s, const uint8_t root[32], int flags, int
 int64_t bsg_reader_read(bsg_reader* r, uint8_t* buf, size_t n); /* bytes; 0 at EOF; <0 error */
 int64_t bsg_reader_seek(bsg_reader* r, int64_t off, int whence);
 uint64_t bsg_reader_size(const bsg_reader* r);
+/* Verify-mode diagnostics: out[0] windows verified on the reading thread, out[1] windows taken
+ * from the background read-ahead, out[2] bytes verified, out[3] read-ahead windows dropped (a
+ * seek made them stale). */
+int bsg_reader_stats(const bsg_reader* r, uint64_t out[4]);
 void bsg_reader_free(bsg_reader* r);
+
+/* ---- test and debug knobs (process-wide; each starts from its environment variable) ---- */
+#define BSG_KNOB_SEQ_WAIT 1      /* BSG_DEBUG_SEQ_WAIT: polls of a k_sha helper handshake before
+                                  * it flags a device error (0: fail at once; tests) */
+#define BSG_KNOB_LONG_MODE 2     /* BSG_LONG_MODE: wave-mode tiers 0 auto, 1 off, 2 all */
+#define BSG_KNOB_VERIFY_WINDOW 3 /* BSG_VERIFY_WINDOW: split::Reader verify window in bytes
+                                  * (0: 256 MiB), read when a Reader is opened */
+int bsg_debug_set(int knob, int64_t value);
+int64_t bsg_debug_get(int knob); /* -1 for an unknown knob */
 
 #ifdef __cplusplus
 }

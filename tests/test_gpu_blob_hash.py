@@ -73,6 +73,30 @@ def test_hasher_runs_around_256mib(gpu, shared_hasher, total_mib, big_mib):
     assert shared_hasher.sum_ptrs(blobs) == [hashlib.sha256(b).digest() for b in blobs]
 
 
+def test_hasher_large_blob_small_path_pins_nothing_big(gpu):
+    """the small-batch path is chosen by blob count, so one large blob
+    (a single Put, a Reader window with a few long chunks) lands there. Its bytes must be
+    copied from pageable memory, not through a blob-sized pinned buffer that the pooled hasher
+    would then hold for the life of the process. A 256 MiB + 1 blob, through bsg_hasher_sum and
+    bsg_hasher_sum_ptrs (one blob, and three blobs), against hashlib; the hasher's pinned
+    memory stays under 8 MiB."""
+    rng = np.random.default_rng(11)
+    big = rng.bytes((256 << 20) + 1)
+    small = [b"", rng.bytes(1000)]
+    h = gpu.Hasher()
+    try:
+        want = hashlib.sha256(big).digest()
+        assert h.sum([big]) == [want]
+        assert h.sum_ptrs([big]) == [want]
+        assert h.sum_ptrs([small[0], big, small[1]]) == [hashlib.sha256(b).digest()
+                                                         for b in (small[0], big, small[1])]
+        assert h.pinned_bytes() < 8 << 20, h.pinned_bytes()
+        # the small path still goes through pinned memory for small blobs, and stays correct
+        assert h.sum(small) == [hashlib.sha256(b).digest() for b in small]
+    finally:
+        h.free()
+
+
 def test_sha256_batch_over_65535_blobs(gpu):
     rng = np.random.default_rng(8)
     lens = rng.integers(0, 160, 70_000)
@@ -111,8 +135,9 @@ def test_engine_hash_device_resident(gpu):
 
 
 @pytest.fixture
-def small_windows(monkeypatch):
-    monkeypatch.setenv("BSG_VERIFY_WINDOW", "65536")
+def small_windows(gpu):
+    with gpu.debug_knob(gpu.KNOB_VERIFY_WINDOW, 65536):
+        yield
 
 
 def test_reader_verify_windows(gpu, small_windows, tmp_path):
@@ -155,3 +180,33 @@ def test_reader_verify_windows(gpu, small_windows, tmp_path):
     with pytest.raises(gpu.BsgError) as ei:
         r.read_all()
     assert ei.value.code == gpu.CORRUPT
+
+
+def test_reader_seek_drops_stale_read_ahead(gpu, small_windows):
+    """a window read ahead before a seek belongs to the old position. The
+    first sequential read after the seek must not take it (that started yet another full window
+    from the old cursor and verified a third on the reading thread): it is dropped, and exactly
+    one window is verified at the new position."""
+    from bs_amd.synth import splitmix_bytes
+    data = splitmix_bytes(43, 3_000_000)
+    st = gpu.MemStore()
+    w = gpu.Writer(st, bits=10, min_size=64, fanout=2)
+    w.write(data)
+    w.close()
+    root = w.root
+    w.free()
+    r = gpu.Reader(st, root, verify=True)
+    assert r.read(200_000) == data[:200_000]  # sequential: windows ahead are started and taken
+    before = r.stats()
+    assert before["ahead_windows"] >= 1 and before["dropped"] == 0
+    pos = 2_000_000
+    assert r.seek(pos, 0) == pos
+    assert r.read(10) == data[pos:pos + 10]   # the seeked leaf node alone
+    assert r.read(8192) == data[pos + 10:pos + 8202]  # sequential again: one new window
+    after = r.stats()
+    assert after["dropped"] == 1, (before, after)
+    assert after["ahead_windows"] == before["ahead_windows"], (before, after)
+    assert after["sync_windows"] == before["sync_windows"] + 2, (before, after)
+    assert r.read(500_000) == data[pos + 8202:pos + 508_202]  # and reads ahead from there
+    assert r.stats()["ahead_windows"] > after["ahead_windows"]
+    r.free()

@@ -119,15 +119,12 @@ def test_eight_writers_one_filestore(gpu, streams, want_roots, tmp_path):
 
     # verifying Readers, concurrently, with small windows so that the background verification
     # and the foreground one overlap across Readers
-    os.environ["BSG_VERIFY_WINDOW"] = str(4 * MiB)
-    try:
+    with gpu.debug_knob(gpu.KNOB_VERIFY_WINDOW, 4 * MiB):
         def read(i):
             seed = JOBS[i][0]
             return gpu.Reader(st, roots[i], verify=True).read_all() == streams[seed].tobytes()
         with ThreadPoolExecutor(len(JOBS)) as ex:
             assert all(ex.map(read, range(len(JOBS))))
-    finally:
-        del os.environ["BSG_VERIFY_WINDOW"]
     st.free()
 
 

@@ -10,8 +10,6 @@ BSG_DEBUG_SEQ_WAIT=0 (read by the library at every run) makes every helper-wave 
 k_sha (lds_seq_wait: the helped solo chains of a lightly loaded launch) give up at once, which
 sets Counters::error exactly as a real ~1 s handshake timeout would.
 """
-import contextlib
-import os
 
 import pytest
 
@@ -21,13 +19,11 @@ MiB = 1 << 20
 EDEVICE = -5
 
 
-@contextlib.contextmanager
 def failing_handshakes():
-    os.environ["BSG_DEBUG_SEQ_WAIT"] = "0"
-    try:
-        yield
-    finally:
-        del os.environ["BSG_DEBUG_SEQ_WAIT"]
+    # a process-wide knob, not the environment: a setenv while library threads run races their
+    # getenv
+    from bs_amd import bsgpu
+    return bsgpu.debug_knob(bsgpu.KNOB_SEQ_WAIT, 0)
 
 
 def test_errstr_names_edevice(gpu):

@@ -374,20 +374,20 @@ def test_streaming_fuzz_vs_oracle(gpu, oracle, table, seed):
 
 
 @pytest.mark.parametrize("mode", ["off", "all"])
-def test_sha_path_forced(gpu, oracle, table, mode, monkeypatch):
+def test_sha_path_forced(gpu, oracle, table, mode):
     """Every job through one SHA-256 path: per-lane only (BSG_LONG_MODE=off) or wave mode only
     (all: solo and group tickets for every eligible job), over streams whose chunks span short
     to very long; both must give the oracle's refs."""
     from bs_amd.synth import splitmix_array
-    monkeypatch.setenv("BSG_LONG_MODE", mode)
     arrs = [splitmix_array(31 + i, n) for i, n in enumerate([0, 5_000, 700_000, 3_000_001])]
-    for bits, mn in ((16, 1024), (13, 64), (18, 4096)):
-        ch, counts = gpu.split_hash_batch(arrs, bits=bits, min_size=mn)
-        k = 0
-        for i, a in enumerate(arrs):
-            one = oracle.split(table, a, bits=bits, min_size=mn)
-            assert as_tuples(ch[k:k + int(counts[i])]) == as_tuples(one), (mode, bits, i)
-            k += int(counts[i])
+    with gpu.debug_knob(gpu.KNOB_LONG_MODE, {"off": 1, "all": 2}[mode]):
+        for bits, mn in ((16, 1024), (13, 64), (18, 4096)):
+            ch, counts = gpu.split_hash_batch(arrs, bits=bits, min_size=mn)
+            k = 0
+            for i, a in enumerate(arrs):
+                one = oracle.split(table, a, bits=bits, min_size=mn)
+                assert as_tuples(ch[k:k + int(counts[i])]) == as_tuples(one), (mode, bits, i)
+                k += int(counts[i])
 
 
 @pytest.mark.parametrize("carry_cap", [None, 0])
