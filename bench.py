@@ -53,7 +53,9 @@ def parse():
                     help="timed steps of the nested configs[2] record (256 x 64 MiB on the same "
                          "GPU, N=1 default run only; default: --steps, 0: skip)")
     ap.add_argument("--check", action="store_true",
-                    help="verify the device records against the CPU oracle after timing")
+                    help="also verify the records against the oracle on bytes generated on the "
+                         "host (checks the device fill too); the default run already checks them "
+                         "against the oracle on the device bytes (the CPU baseline's sample)")
     a = ap.parse_args()
     if a.configs2_steps is None:
         a.configs2_steps = a.steps
@@ -137,14 +139,18 @@ def cpu_threads() -> int:
     return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
 
 
-def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str) -> dict | None:
+def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str):
     """The C oracle ("port" of the reference's per-stream Splitter + sha256: literal per-byte
     buzhash32 loop, SHA-256 with the x86 SHA extensions when the host has them, as Go's amd64
     crypto/sha256 does) over a bounded sample of the same bytes on this host. One stream per
     thread, as the reference runs one goroutine per stream: 1 thread for a single stream,
-    cpu_threads() for a batch."""
+    cpu_threads() for a batch. It is NOT Go's split.Writer: the per-byte loop is a tight C
+    register loop (oracle/bsoracle.c), likely faster than hashsplit's append + Roll per byte, so
+    the stated CPU rate is an optimistic stand-in for the reference (Go is absent here and on
+    the GPU box). Returns (baseline record, the oracle's chunks of the sample): the chunks are
+    the parity check of the device records on the same bytes."""
     if not host_streams:
-        return None
+        return None, None
     import numpy as np
     from oracle import oracle as O  # checker / baseline only
     table = O.buzhash32_table(1)
@@ -167,10 +173,11 @@ def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str) -> d
         dt = time.perf_counter() - t0
         nch = len(ch)
     full = cpu_full_writer(O, table, host_streams, bits, min_size, threads)
-    return {"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} (same bytes/params), C oracle split + sha256 ({impl}), "
-                      f"{threads} thread(s), one stream per thread, {nch} chunks in {dt:.2f}s",
-            "full_writer": full}
+    return ({"value": round(n / dt / 2**30, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+             "sample": f"{sample} (same bytes/params), C oracle split + sha256 ({impl}), "
+                       f"{threads} thread(s), one stream per thread, {nch} chunks in {dt:.2f}s",
+             "loop": "tight C restatement of hashsplit's per-byte loop, not Go's Splitter",
+             "full_writer": full}, ch)
 
 
 def cpu_full_writer(O, table, host_streams: list, bits: int, min_size: int, threads: int) -> dict:
@@ -255,6 +262,16 @@ KERNEL_NAMES = {"k_scan": ("void bsg::k_scan<true>(bsg::ScanArgs)",
                           "bsg::k_sha(bsg::ShaArgs)")}  # (one kernel before the split)
 
 
+def same_workload(doc_w: str, workload: str) -> bool:
+    """A PMC summary belongs to this line's workload: the same BASELINE config ("configs[k]"
+    before the colon), or the same name exactly. Empty or generic names never match."""
+    if not doc_w or not workload:
+        return False
+    if doc_w.startswith("configs[") and workload.startswith("configs["):
+        return doc_w.split(":", 1)[0] == workload.split(":", 1)[0]
+    return doc_w == workload
+
+
 def pmc_traffic(kernel: str, workload: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary for this workload
     (profiles/rNN_pmc.json, written by tools/pmc_summary.py from rocprofv3 FETCH_SIZE and
@@ -267,7 +284,7 @@ def pmc_traffic(kernel: str, workload: str):
                 doc = json.load(f)
         except (OSError, ValueError):
             continue
-        if doc.get("workload", "\0") not in workload:
+        if not same_workload(doc.get("workload") or "", workload):
             continue
         ks = [doc.get("kernels", {}).get(n) for n in names]
         ks = [k for k in ks if k]
@@ -325,35 +342,78 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
     nsteps[0] = 0
     elapsed = timed_steps(step, sync, world, steps, 0)
     stage_avg = [s / max(nsteps[0], 1) for s in stage_sum]
-    ok = None
-    if check and rank == 0:
+    diag = eng.diag()
+    chunks = int(eng.nchunks)
+    # the last timed step's records, copied to the host after timing: checked below against
+    # the oracle on the same device bytes (the metric's "chunk/ref bit-parity" half)
+    dev_ch = eng.chunks()
+    dev_counts = eng.counts() if ns > 1 else None
+    gen_ok = None
+    if check and rank == 0:  # --check: also against bytes generated on the host (checks the fill)
         from bs_amd.synth import splitmix_array
         from oracle import oracle as O  # checker only, after timing
         ref = O.split(O.buzhash32_table(1), splitmix_array(BASE_SEED, nbytes), bits=bits,
                       min_size=min_size)
-        got = eng.chunks()[: len(ref)] if ns == 1 else eng.chunks()[: eng.counts()[0]]
-        ok = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
-                  and (got["offset"] == ref["offset"]).all())
-    diag = eng.diag()
-    chunks = int(eng.nchunks)
+        got = dev_ch[: len(ref)] if ns == 1 else dev_ch[: int(dev_counts[0])]
+        gen_ok = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
+                      and (got["offset"] == ref["offset"]).all())
     # the CPU baseline's sample: the same device bytes, copied back after timing
-    host_streams, sample = [], ""
+    host_streams, sample, full_prefix = [], "", True
     if rank == 0 and world == 1 and cpu_sample > 0:
         want = cpu_sample << 20
         if ns == 1:
             host_streams = [buf.to_host(0, min(nbytes, want))]
+            full_prefix = len(host_streams[0]) == nbytes
             sample = f"first {len(host_streams[0]) >> 20} MiB of stream 0"
         else:
             k = min(ns, max(4 * cpu_threads(), -(-want // nbytes)))
             host_streams = [buf.to_host(offs[i], nbytes) for i in range(k)]
             sample = f"streams 0..{k - 1} of {ns} ({k} x {nbytes >> 20} MiB)"
+    check_streams = []
+    if world > 1 and ns == 1:  # N>1: every rank checks its own stream (no CPU baseline there)
+        check_streams = [buf.to_host(0, nbytes)]
     # the engine and its input are done with: free them before the next leg
     eng.close()
     buf.free()
-    cpu = cpu_baseline(host_streams, bits, min_size, sample)
+    cpu, ref_ch = cpu_baseline(host_streams, bits, min_size, sample)
     del host_streams
+    ok, checked = None, ""
+    if ref_ch is not None:
+        ok = records_match(dev_ch, dev_counts, ref_ch, ns, full_prefix)
+        checked = sample
+    elif check_streams:
+        from oracle import oracle as O  # checker only, after timing
+        ref_ch = O.split(O.buzhash32_table(1), check_streams[0], bits=bits, min_size=min_size)
+        ok = records_match(dev_ch, None, ref_ch, 1, True)
+        checked = f"rank {rank}'s whole stream"
+    del check_streams
+    if world > 1 and ok is not None:  # all ranks' checks
+        ok = max_over_ranks(0.0 if ok else 1.0, world) == 0.0
+        checked = "every rank's whole stream"
+    if gen_ok is not None:
+        ok = gen_ok if ok is None else (ok and gen_ok)
     return {"elapsed": elapsed, "stage_avg": stage_avg, "diag": diag, "chunks": chunks,
-            "check": ok, "cpu": cpu}
+            "check": ok, "checked": checked, "cpu": cpu}
+
+
+def records_match(dev, dev_counts, ref, ns: int, full: bool) -> bool:
+    """Device records == the oracle's, bit for bit (offset, len, level, stream, ref). ns == 1:
+    the oracle split a prefix of the stream (full: the whole stream; else its last chunk is the
+    prefix's forced final one and is not compared). ns > 1: the oracle split whole streams
+    0..k-1, which are the first counts[0..k) device records."""
+    import numpy as np
+    if ns == 1:
+        n = len(ref) if full else len(ref) - 1
+        if (full and len(dev) != n) or len(dev) < n:
+            return False
+        d, r = dev[:n], ref[:n]
+    else:
+        k = len(np.unique(ref["stream"])) if len(ref) else 0
+        n = int(dev_counts[:k].sum())
+        if n != len(ref):
+            return False
+        d, r = dev[:n], ref
+    return all(bool((d[f] == r[f]).all()) for f in ("offset", "len", "level", "stream", "ref"))
 
 
 def roofline(workload: str, per_launch_bytes: int, stage_avg: list) -> dict:
@@ -399,6 +459,7 @@ def main():
         leg2 = device_leg(ns2, n2, 16, 1024, args.configs2_steps, args.warmup, 1, 0, local,
                           args.cpu_sample_mib, False)
         c2 = {"workload": CONFIGS2,
+              "oracle_check": leg2["check"], "oracle_checked": leg2["checked"],
               "value": round(ns2 * n2 * args.configs2_steps / leg2["elapsed"] / 2**30, 3),
               "unit": "GiB/s", "steps": args.configs2_steps, "warmup": args.warmup,
               "ms_per_step": round(leg2["elapsed"] * 1e3 / args.configs2_steps, 3),
@@ -436,8 +497,8 @@ def main():
             "chain_roofline": chain_roofline(leg["diag"]),
             "configs2": c2,
         }
-        if leg["check"] is not None:
-            line["oracle_check"] = leg["check"]
+        line["oracle_check"] = leg["check"]
+        line["oracle_checked"] = leg["checked"]
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -1158,8 +1158,11 @@ struct bsg_ctx {
     if ((rc0 = ensure_slot(i))) return rc0;
     TileSlot& t = slots[i];
     bsg_engine* e = t.eng;
-    // the engine of the tile kSlots back: its records must be collected before the engine's
-    // buffers are reused (the H2Ds above already queue behind its kernels on the same stream)
+    // Two invariants keep a tile's buffers safe. reclaim(i) protects the ENGINE's work buffers:
+    // the records of the tile kSlots back on this engine are collected before its buffers are
+    // reused. The DATA slot is protected by copy_prepare() and its free_ev: the H2D copies run
+    // on the context's copy stream (cstream), which waits for the event recorded after the last
+    // kernels (and the carry copy) that read the slot, before refilling it.
     rc0 = reclaim(i);
     if (rc0) return rc0;
     if ((rc0 = copy_prepare())) return rc0;

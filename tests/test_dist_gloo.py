@@ -50,6 +50,16 @@ def _worker(rank, world, port, q):
         out["chunks"] = O.split(table, data)
 
     elapsed = bench.timed_steps(step, lambda: None, w, steps=2, warmup=1)
+    # the bench's per-rank parity check and its reduction over ranks: both ranks see rank 1's
+    # tampered record
+    ok = bench.records_match(out["chunks"], None, O.split(table, data), 1, True)
+    all_ok = bench.max_over_ranks(0.0 if ok else 1.0, w) == 0.0
+    bad = out["chunks"].copy()
+    if r == 1:
+        bad["ref"][len(bad) // 2, 0] ^= 1
+    ok_bad = bench.records_match(bad, None, O.split(table, data), 1, True)
+    all_bad = bench.max_over_ranks(0.0 if ok_bad else 1.0, w) == 0.0
+    assert ok and all_ok and not all_bad
     q.put((r, elapsed, len(out["chunks"]), int(out["chunks"]["len"].sum())))
     import torch.distributed as dist
     dist.destroy_process_group()
@@ -117,3 +127,33 @@ def test_bench_refuses_wrong_gpu_count():
                        capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_records_match_prefix_and_batch():
+    """bench.records_match, the check behind the bench line's oracle_check: a single stream
+    checked on a prefix (the oracle's forced last chunk is not compared), and a batch whose
+    first k streams the oracle split whole."""
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from bs_amd.synth import splitmix_array
+    from oracle import oracle as O
+    table = O.buzhash32_table(1)
+    d = splitmix_array(5, 3 << 20)
+    full = O.split(table, d)
+    assert bench.records_match(full, None, full, 1, True)
+    pre = O.split(table, d[: 1 << 20])          # a prefix: its last chunk is forced
+    assert bench.records_match(full, None, pre, 1, False)
+    assert not bench.records_match(full, None, pre, 1, True)
+    streams = [splitmix_array(9 + i, 300_000 + 7 * i) for i in range(4)]
+    lens = [len(a) for a in streams]
+    base = np.concatenate(streams)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    dev, counts = O.split_streams(table, base, off, lens, threads=2)
+    ref, _ = O.split_streams(table, base[: int(off[2])], off[:2], lens[:2], threads=2)
+    assert bench.records_match(dev, counts, ref, 4, True)
+    dev2 = dev.copy()
+    dev2["level"][1] += 1
+    assert not bench.records_match(dev2, counts, ref, 4, True)

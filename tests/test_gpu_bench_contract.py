@@ -42,6 +42,7 @@ def test_bench_json_line():
     assert cb["kind"] in ("port", "reference") and cb["sample"]
     assert d["end_to_end"]["value"] > 0
     assert d["chain_roofline"]["frac"] > 0
+    assert d["oracle_check"] is True and d["oracle_checked"]  # parity on the bench's own bytes
 
 
 @pytest.mark.gpu
@@ -62,3 +63,4 @@ def test_bench_default_carries_configs2():
     assert c2["roofline"]["k_scan"]["frac"] > 0
     assert c2["cpu_baseline"]["cores"] >= 1 and c2["cpu_baseline"]["full_writer"]["value"] > 0
     assert set(c2["stage_ms"]) == set(d["stage_ms"])
+    assert d["oracle_check"] is True and c2["oracle_check"] is True
