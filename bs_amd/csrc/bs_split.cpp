@@ -673,7 +673,6 @@ static std::shared_ptr<uint8_t> alloc_piece(size_t n) {
     void* m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
       (void)::madvise(m, len, MADV_HUGEPAGE);
-      bsg::numa_place(m, len);  // read by DMA (staging copies) and the verifying Reader
       return std::shared_ptr<uint8_t>(static_cast<uint8_t*>(m),
                                       [len](uint8_t* q) { ::munmap(q, len); });
     }

@@ -122,7 +122,6 @@ struct PinBuf {
       void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
       if (m != MAP_FAILED) {
         (void)::madvise(m, n, MADV_HUGEPAGE);
-        bsg::numa_place(m, n);  // registering faults the pages in: on the device's node
         if (hipHostRegister(m, n, hipHostRegisterDefault) == hipSuccess) {
           *q = m;
           *len = n;
@@ -179,37 +178,28 @@ int herr(hipError_t e) { return e == hipSuccess ? BSG_OK : BSG_EDEVICE; }
 // an engine per tile slot paid every time. Streams go back to the pool instead.
 constexpr size_t kStreamPoolMax = 32;
 std::mutex g_stream_mu;
-// `prio`: a separate pool of streams at the device's greatest priority (the runtime gives them
-// hardware queues of their own), for short synchronous work that must not wait in a queue
-// behind a long k_sha (the split::Writer's tree-node hashes).
-std::vector<hipStream_t>& stream_pool(int device, bool prio) {
-  static auto* pools = new std::vector<std::vector<hipStream_t>>(128);  // never destroyed
-  return (*pools)[((size_t)device & 63) * 2 + (prio ? 1 : 0)];
+std::vector<hipStream_t>& stream_pool(int device) {
+  static auto* pools = new std::vector<std::vector<hipStream_t>>(64);  // never destroyed
+  return (*pools)[(size_t)device & 63];
 }
-hipError_t stream_acquire(int device, hipStream_t* s, bool prio = false) {
+hipError_t stream_acquire(int device, hipStream_t* s) {
   {
     std::lock_guard<std::mutex> g(g_stream_mu);
-    auto& v = stream_pool(device, prio);
+    auto& v = stream_pool(device);
     if (!v.empty()) {
       *s = v.back();
       v.pop_back();
       return hipSuccess;
     }
   }
-  if (prio) {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
-    (void)hipGetLastError();
-  }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 // The stream must be idle (callers synchronise it first); the device must be current.
-void stream_release(int device, hipStream_t s, bool prio = false) {
+void stream_release(int device, hipStream_t s) {
   if (!s) return;
   {
     std::lock_guard<std::mutex> g(g_stream_mu);
-    auto& v = stream_pool(device, prio);
+    auto& v = stream_pool(device);
     if (v.size() < kStreamPoolMax) {
       v.push_back(s);
       return;
@@ -645,9 +635,6 @@ class CopyPool {
   explicit CopyPool(int workers) {
     for (int i = 0; i < workers; ++i) th_.emplace_back([this] { Work(); });
   }
-  void Bind(const cpu_set_t& cpus) {
-    for (std::thread& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof cpus, &cpus);
-  }
   void Run(size_t n, const std::function<void(size_t)>& fn) {
     auto job = std::make_shared<PoolJob>();
     job->fn = &fn;
@@ -706,84 +693,6 @@ void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
     return;
   }
   copy_pool()->Run(n, fn);
-}
-
-namespace {
-std::atomic<int> g_numa_node{-1};
-
-// The NUMA node of a device's PCI function, from sysfs (-1: unknown, e.g. one-node hosts).
-int device_numa_node(int device) {
-  char bus[64] = {0};
-  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
-    (void)hipGetLastError();
-    return -1;
-  }
-  for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
-  char path[160];
-  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
-  FILE* f = std::fopen(path, "r");
-  if (!f) return -1;
-  int node = -1;
-  if (std::fscanf(f, "%d", &node) != 1) node = -1;
-  std::fclose(f);
-  return node;
-}
-
-// The CPUs of `node` this process may run on (false if none, or the node is unknown).
-bool node_cpus(int node, cpu_set_t* out) {
-  char path[96];
-  std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
-  FILE* f = std::fopen(path, "r");
-  if (!f) return false;
-  cpu_set_t allowed;
-  CPU_ZERO(&allowed);
-  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) {
-    std::fclose(f);
-    return false;
-  }
-  CPU_ZERO(out);
-  int a, b, n = 0;
-  while (std::fscanf(f, "%d", &a) == 1) {
-    b = a;
-    int c = std::fgetc(f);
-    if (c == '-') {
-      if (std::fscanf(f, "%d", &b) != 1) break;
-      c = std::fgetc(f);
-    }
-    for (int k = a; k <= b && k < CPU_SETSIZE; ++k)
-      if (CPU_ISSET(k, &allowed)) {
-        CPU_SET(k, out);
-        ++n;
-      }
-    if (c != ',') break;
-  }
-  std::fclose(f);
-  return n > 0;
-}
-}  // namespace
-
-void numa_setup(int device) {
-  static std::once_flag once;
-  std::call_once(once, [device] {
-    const char* e = std::getenv("BSG_NUMA");
-    if (!e || std::atoi(e) == 0) return;  // opt-in: measured no gain on the MI355X box
-    const int node = device_numa_node(device);
-    cpu_set_t cpus;
-    if (node < 0 || !node_cpus(node, &cpus)) return;
-    g_numa_node.store(node);
-    if (CopyPool* pool = copy_pool()) pool->Bind(cpus);
-    if (std::getenv("BSG_DEBUG_NUMA"))
-      std::fprintf(stderr, "bsgpu: device %d on NUMA node %d (%d CPUs)\n", device, node,
-                   CPU_COUNT(&cpus));
-  });
-}
-
-void numa_place(void* p, size_t len) {
-  const int node = g_numa_node.load();
-  if (node < 0 || node >= 64 || !p || !len) return;
-  const unsigned long mask = 1ul << node;
-  constexpr int kMpolPreferred = 1;  // numaif.h MPOL_PREFERRED (no libnuma dependency)
-  (void)syscall(SYS_mbind, p, len, kMpolPreferred, &mask, 64ul, 0u);
 }
 
 }  // namespace bsg
@@ -849,10 +758,6 @@ class StagePool {
     return *p;
   }
   bool take(PinBuf* out) {  // out: empty
-#ifdef BSG_NO_STAGE_POOL  // experiment switch (tools/writer_ab.py): every context pins its own
-    (void)out;
-    return false;
-#endif
     std::lock_guard<std::mutex> g(mu_);
     if (free_.empty()) return false;
     *out = free_.back();
@@ -861,11 +766,7 @@ class StagePool {
   }
   void give(PinBuf* b) {  // takes b's buffer if it is a full-size one; b is empty afterwards
     if (!b->p) return;
-#ifdef BSG_NO_STAGE_POOL
-    if (false) {
-#else
     if (b->cap >= kStageMax && b->map_len) {
-#endif
       std::lock_guard<std::mutex> g(mu_);
       if (free_.size() < kMaxFree) {
         free_.push_back(*b);
@@ -877,10 +778,6 @@ class StagePool {
     b->release();
   }
   int fill(int n) {  // bsg_init: make sure n full-size stages are pinned and waiting
-#ifdef BSG_NO_STAGE_POOL
-    (void)n;
-    return BSG_OK;
-#endif
     for (;;) {
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -1472,7 +1369,6 @@ void bsg_default_table(uint32_t out[256]) { std::memcpy(out, kBuzhash32Seed1, 10
 int bsg_init(int device) {
   if (device < 0 || device >= bsg_device_count()) return BSG_ENODEV;
   HCHECK(hipSetDevice(device));
-  bsg::numa_setup(device);
   // streams for the pool. The first four get the process's hardware queues (GPU_MAX_HW_QUEUES,
   // 4); every further one still costs ~2.4 ms to create, and each live split::Writer holds
   // three (its hasher's, its first engine's, its copy stream): a Writer opened while others are
@@ -1532,9 +1428,7 @@ int bsg_init(int device) {
   if (rc) return rc;
   bsg::parallel_for(bsg::copy_threads(), [](size_t) {});  // the host copy pool's threads
   // a ring's worth of full-size pinned stages for the first large stream
-#ifndef BSG_NO_INIT_STAGES  // experiment switch: no stages pinned ahead
   if ((rc = StagePool::get().fill(kStages))) return rc;
-#endif
   // the streaming path once (registered staging, H2D from it, kernels writing into mapped
   // host memory, events): first uses the process would otherwise pay in its first Writer
   bsg_ctx* c = bsg_open(device, nullptr, nullptr, &rc);
@@ -1768,7 +1662,6 @@ bsg_ctx* bsg_open(int device, const bsg_params* params, const uint32_t* table, i
     *err = BSG_ENODEV;
     return nullptr;
   }
-  bsg::numa_setup(device);
   bsg_ctx* c = new (std::nothrow) bsg_ctx();
   if (!c) {
     *err = BSG_ENOMEM;
@@ -2146,7 +2039,6 @@ struct bsg_hasher {
   int dev = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
-  bool prio = false;  // stream from the high-priority pool (BSG_HASHER_PRIO)
   DevBuf data, off, len, refs;
   PinBuf h_meta;  // off[n] | len[n] staged for one H2D
   PinBuf h_small; // a small batch's host bytes, then its refs: pinned, so both copies are DMA
@@ -2285,17 +2177,11 @@ extern "C" {
 bsg_hasher* bsg_hasher_new(int device) {
   if (device < 0 || device >= bsg_device_count() || hipSetDevice(device) != hipSuccess)
     return nullptr;
-  bsg::numa_setup(device);
   bsg_hasher* h = new (std::nothrow) bsg_hasher();
   if (!h) return nullptr;
   h->dev = device;
   h->num_cus = device_cus(device);
-  static const bool prio = [] {
-    const char* e = std::getenv("BSG_HASHER_PRIO");
-    return e && std::atoi(e) != 0;
-  }();
-  h->prio = prio;
-  if (stream_acquire(device, &h->stream, h->prio) != hipSuccess) {
+  if (stream_acquire(device, &h->stream) != hipSuccess) {
     delete h;
     return nullptr;
   }
@@ -2353,7 +2239,7 @@ void bsg_hasher_free(bsg_hasher* h) {
   h->h_recs.release();
   h->dstage.release();
   if (h->eng) bsg_engine_destroy(h->eng);
-  if (h->stream) stream_release(h->dev, h->stream, h->prio);
+  if (h->stream) stream_release(h->dev, h->stream);
   delete h;
 }
 

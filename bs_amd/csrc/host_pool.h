@@ -18,13 +18,4 @@ int copy_threads();
 // have run. fn must not call parallel_for itself.
 void parallel_for(size_t n, const std::function<void(size_t)>& fn);
 
-// NUMA placement of the host side (BSG_NUMA=1, opt-in): the first device a process opens
-// names the node its PCIe link hangs off; the pool's threads run on that node's CPUs and the
-// buffers the device reads by DMA (staging, Write pieces) get their pages there. On the shared
-// two-node MI355X box it measured no gain, so it is off by default.
-void numa_setup(int device);
-// Asks the kernel to place [p, p + len) (an anonymous mapping not yet touched) on that node;
-// a no-op before numa_setup or without a known node.
-void numa_place(void* p, size_t len);
-
 }  // namespace bsg
