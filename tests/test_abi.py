@@ -73,3 +73,24 @@ def test_errstr_and_bad_device():
         else:
             assert h and err.value == 0
             L.bsg_free(h)
+
+
+def test_debug_knobs_and_null_handles():
+    """bsg_debug_set / bsg_debug_get (the test knobs that replaced run-time getenv)
+    and the round-4 entry points on null handles: no GPU needed."""
+    from bs_amd import bsgpu
+    L = bsgpu.lib()
+    for knob in (bsgpu.KNOB_SEQ_WAIT, bsgpu.KNOB_LONG_MODE, bsgpu.KNOB_VERIFY_WINDOW):
+        old = bsgpu.debug_get(knob)
+        assert old >= 0
+        with bsgpu.debug_knob(knob, 1):
+            assert bsgpu.debug_get(knob) == 1
+        assert bsgpu.debug_get(knob) == old
+    assert L.bsg_debug_set(bsgpu.KNOB_LONG_MODE, 3) == -22   # 0 auto, 1 off, 2 all
+    assert L.bsg_debug_set(bsgpu.KNOB_SEQ_WAIT, -1) == -22
+    assert L.bsg_debug_set(99, 0) == -22 and L.bsg_debug_get(99) == -1
+    out = np.zeros(4, dtype=np.uint64)
+    assert L.bsg_reader_stats(None, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == -22
+    assert L.bsg_set_stream_base(None, 1 << 40) == -22
+    assert L.bsg_writer_set_stream_base(None, 1 << 40) == -22
+    assert L.bsg_hasher_pinned_bytes(None) == 0

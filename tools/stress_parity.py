@@ -1,7 +1,9 @@
 """Long randomized parity run (not part of pytest): many seeded draws of batch splits, streaming
 splits and (round 3) C++ split.Writer runs with small and large Writes mixed, against the
 oracle. python tools/stress_parity.py [N] [seed_base] -- prints a line per 20 draws.
-STRESS_WRITER=0 restores the round-1/2 mix (batch and streaming draws only)."""
+STRESS_WRITER=0 restores the round-1/2 mix (batch and streaming draws only). Round 4: a third of
+the streaming and Writer draws start their stream at a random offset past 2^40
+(bsg_set_stream_base): streaming records must be the oracle's shifted by it, Writer Roots equal."""
 import os
 import sys
 import time
@@ -38,6 +40,8 @@ def main():
             fo = int(rng.choice([2, 4, 8]))
             st = bsgpu.MemStore()
             w = bsgpu.Writer(st, bits=bits, min_size=mn, fanout=fo, tile=tile)
+            if rng.random() < 1 / 3:
+                w.set_stream_base(int(rng.integers(1 << 40, 1 << 50)))
             mv = memoryview(data)
             pos = 0
             while pos < n:
@@ -65,6 +69,9 @@ def main():
             data = splitmix_bytes(2_000_000 + d, n)
             tile = int(rng.choice([65536, 1 << 20, 16 << 20]))
             w = bsgpu.StreamingSplitter(bits=bits, min_size=mn, tile=tile)
+            base = int(rng.integers(1 << 40, 1 << 50)) if rng.random() < 1 / 3 else 0
+            if base:
+                w.set_stream_base(base)
             pos, got = 0, []
             while pos < n:
                 k = int(rng.choice([4096, 100_000, 4 << 20]))
@@ -74,8 +81,9 @@ def main():
             w.close()
             got.append(w.drain())
             w.free()
-            want = tuples(O.split(table, np.frombuffer(data, dtype=np.uint8), bits=bits, min_size=mn))
-            assert tuples(np.concatenate(got)) == want, ("stream", d, bits, mn, n, tile)
+            want = [(o + base, ln, lv, r) for o, ln, lv, r in
+                    tuples(O.split(table, np.frombuffer(data, dtype=np.uint8), bits=bits, min_size=mn))]
+            assert tuples(np.concatenate(got)) == want, ("stream", d, bits, mn, n, tile, base)
         if d % 20 == 19:
             print(f"{d + 1} draws ok ({time.time() - t0:.0f} s)", flush=True)
     print(f"all {n_draws} draws bit-identical to the oracle", flush=True)
