@@ -13,6 +13,11 @@ measured 1.115 us per 64-byte block; a chain can never end before its chunk's en
   stage16   per 16 MiB
   start     the ideal: as soon as the chunk's first byte has landed
 
+Then the tile-size sweep of today's pipeline: tile t runs on engine t mod 3 (three tiles in
+flight) once it has landed and that engine's previous tile has finished; a chunk's chain starts
+after the scan of the tile it closes in (an open chunk is carried into the next tile) and the
+tile ends with its longest chain.
+
   python tools/sim_e2e_tail.py [--gib 1 4] [--h2d-gbs 57] [--us-per-block 1.115]
 """
 import argparse
@@ -52,6 +57,18 @@ def main() -> None:
             print(f"  {name:8s} last chain ends {end.max() * 1e3:7.2f} ms = "
                   f"{n / end.max() / 2**30:5.1f} GiB/s (chunk of {ln[i] / 1e3:.0f} KB at "
                   f"{off[i] / 2**20:.0f} MiB)")
+        cend = (off + ln).astype(np.int64)
+        for tile_mib in (64, 128, 192, 256, 320, 512):
+            tile = tile_mib << 20
+            ntiles = -(-n // tile)
+            t_of = (cend - 1) // tile
+            tend = np.zeros(ntiles)
+            for t in range(ntiles):
+                st = max(min((t + 1) * tile, n) / h2d, tend[t - 3] if t >= 3 else 0.0)
+                sel = t_of == t
+                tend[t] = st + args.scan_ms * 1e-3 + (chain[sel].max() if sel.any() else 0.0)
+            print(f"  today's pipeline, tile {tile_mib:3d} MiB: {tend.max() * 1e3:7.2f} ms = "
+                  f"{n / tend.max() / 2**30:5.1f} GiB/s")
 
 
 if __name__ == "__main__":
