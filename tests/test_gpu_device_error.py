@@ -6,9 +6,10 @@ The reference has no device, but its error convention is the one kept here (SURV
 panics; a failure inside the chunker or a Put propagates out of Write / Close as an error
 (split/split.go:99-126), and the caller may start over.
 
-BSG_DEBUG_SEQ_WAIT=0 (read by the library at every run) makes every helper-wave handshake of
-k_sha (lds_seq_wait: the helped solo chains of a lightly loaded launch) give up at once, which
-sets Counters::error exactly as a real ~1 s handshake timeout would.
+The test knob BSG_KNOB_SEQ_WAIT = 0 (bsg_debug_set; BSG_DEBUG_SEQ_WAIT in the environment is only
+its starting value) makes every helper-wave handshake of k_sha (lds_seq_wait: the helped solo
+chains of a lightly loaded launch) give up at once, which sets Counters::error exactly as a real
+~1 s handshake timeout would.
 """
 
 import pytest
