@@ -1028,7 +1028,7 @@ struct bsg_ctx {
       st.inflight = false;
     }
     const size_t full = stage_size();
-    const bool big = pos + fill >= full;  // past a stage's worth of bytes: whole stages
+    const bool big = pos - stream0 + fill >= full;  // past a stage's worth: whole stages
     const size_t want = big ? full : std::min(full, std::max(need, kMinStaging));
     const size_t have = std::min(st.buf.cap, full);
     if (have >= want) return BSG_OK;
