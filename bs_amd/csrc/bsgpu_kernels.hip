@@ -2190,9 +2190,12 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
   return (uint32_t)(g < cap ? g : cap);
 }
 
+#ifndef BSG_SCAN_GRID
+#define BSG_SCAN_GRID 2  // k_scan workgroups per CU in the grid (one is resident at a time)
+#endif
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
   const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
-  const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
+  const uint32_t grid = grid_for(groups, 1, (uint32_t)BSG_SCAN_GRID * (uint32_t)num_cus);
   if (a.p.split_bits >= 16)
     hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
   else
