@@ -233,21 +233,25 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     mv = memoryview(data)
     piece = 32 << 20
     w = bsgpu.StreamingSplitter(bits=bits, min_size=min_size, device=device)
-    best, nch = None, 0
+    best, nch, recs = None, 0, []
     for rep in range(4):  # rep 0 grows the pinned staging; best of the other three
         w.reset()
+        recs = []
         t0 = time.perf_counter()
-        nch = 0
         for i in range(0, n, piece):
             w.write(mv[i:i + piece])
-            nch += len(w.drain())
+            recs.append(w.drain())
         w.close()
-        nch += len(w.drain())
+        recs.append(w.drain())
         dt = time.perf_counter() - t0
         if rep and (best is None or dt < best):
             best = dt
     w.free()
+    import numpy as np
+    last = np.concatenate(recs)  # the last rep's records: checked against the oracle in main()
+    nch = len(last)
     return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "chunks": nch,
+            "records": last,
             "path": "host memory -> bsg_write (ring of 4 x 64 MiB pinned stages, each copied "
                     "H2D as it fills, on a copy stream into 4 device data slots) -> split + "
                     "SHA-256 on 3 engines -> records in host memory; tile 256 MiB"}
@@ -393,7 +397,8 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
     if gen_ok is not None:
         ok = gen_ok if ok is None else (ok and gen_ok)
     return {"elapsed": elapsed, "stage_avg": stage_avg, "diag": diag, "chunks": chunks,
-            "check": ok, "checked": checked, "cpu": cpu}
+            "check": ok, "checked": checked, "cpu": cpu,
+            "ref": ref_ch if (ns == 1 and full_prefix) else None}
 
 
 def records_match(dev, dev_counts, ref, ns: int, full: bool) -> bool:
@@ -470,6 +475,13 @@ def main():
               "chain_roofline": chain_roofline(leg2["diag"])}
     e2e = end_to_end(args.e2e_mib, args.bits, args.min_size, local) \
         if (rank == 0 and world == 1) else None
+    if e2e is not None:
+        # the e2e stream is the same SplitMix64 stream as configs[1]'s (seed BASE_SEED): when the
+        # device leg's oracle split covered that whole stream, the host-path records are checked
+        # against it too (bsg_write -> records in host memory, bit for bit)
+        recs, ref = e2e.pop("records"), leg.get("ref")
+        if ref is not None and e2e["bytes"] == nbytes:
+            e2e["oracle_check"] = records_match(recs, None, ref, 1, True)
     if rank == 0:
         line = {
             "metric": METRIC,
