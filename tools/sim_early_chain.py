@@ -75,6 +75,7 @@ def main() -> None:
                     help="jobs this long go to wave tickets (bench sha_path.long_thresh)")
     ap.add_argument("--tickets", type=int, default=240, help="wave tickets (sha_path)")
     ap.add_argument("--simds", type=int, default=1024)
+    ap.add_argument("--clock-ghz", type=float, default=2.31, help="k_sha's loaded clock")
     args = ap.parse_args()
 
     a = chunk_table(args.streams, args.stream_mib, args.threads)
@@ -124,6 +125,35 @@ def main() -> None:
               f"{args.scan_ms + args.sel_ms + t_sha:.2f} ms")
     print("  a step can end no earlier than the larger of the chain bound of its schedule and "
           "the work bound")
+
+    # Round 4: the hash work with k_sha's actual tiers and their measured costs (wave-cycles per
+    # block, DESIGN §4.4: per-lane 6,870 cycles per 64 blocks under full load; pair tickets ~133;
+    # group (octet) tickets ~380; a solo chain holds its wave for 2,702 cycles per block), at the
+    # loaded clock. It is what k_sha's whole chip has to do while the longest chain runs.
+    mx = int(nb.max())
+    order = np.argsort(-nb)
+    solo = np.zeros(len(nb), dtype=bool)
+    solo[order[:16]] = True
+    grp = (nb >= mx * 0.50) & ~solo
+    pair = (nb >= mx * 0.34) & (nb < mx * 0.50)
+    lane = nb < mx * 0.34
+    ghz = args.clock_ghz
+    tiers = (("per-lane", lane, 6870 / 64), ("pair tickets", pair, 133.0),
+             ("group tickets", grp, 380.0), ("solo chains", solo, 2702.0))
+    total = 0.0
+    print(f"tiered hash work at {ghz} GHz on {args.simds} SIMDs (full-chip ms):")
+    for name, m, cyc in tiers:
+        ms = float(nb[m].sum()) * cyc / args.simds / (ghz * 1e6)
+        total += ms
+        print(f"  {name:14s} {int(m.sum()):7d} jobs {nb[m].sum() / 1e6:7.2f} M blocks "
+              f"x {cyc:6.0f} cycles = {ms:6.2f} ms")
+    chain = mx * 2702 / (ghz * 1e6)
+    print(f"  hash work {total:.2f} ms against the longest chain {chain:.2f} ms: the two bounds "
+          f"of k_sha coincide (measured k_sha 14.03 ms, driver round 3)")
+    q = (nb >= mx * 0.50) & (nb < mx * 0.74) & ~solo
+    saved = float(nb[q].sum()) * (380.0 - 190.0) / args.simds / (ghz * 1e6)
+    print(f"  a quad tier (16 chains per wave, ~190 cycles per block) for the jobs between 0.50 and "
+          f"0.74 x the longest would save {saved:.2f} ms of it")
 
 
 if __name__ == "__main__":
