@@ -183,7 +183,7 @@ def _p(a: np.ndarray, ct):
     return a.ctypes.data_as(ctypes.POINTER(ct))
 
 
-KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW = 1, 2, 3  # bsg_debug_set knobs
+KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY = 1, 2, 3, 4  # bsg_debug_set knobs
 
 
 def debug_get(knob: int) -> int:
@@ -434,10 +434,11 @@ class Engine:
                "nshort": int(d[13]), "wave_tickets": int(d[14]), "total_blocks": int(d[15])}
         t = np.zeros(4, dtype=np.uint64)
         _check(lib().bsg_engine_timeline(self.h, _p(t, ctypes.c_uint64)), "bsg_engine_timeline")
-        if t[0] and t[1] and t[3]:  # microseconds after the first k_sha wave started
-            out["timeline_us"] = {"long_start": round(float(t[1] - t[0]) * 0.01, 1),
-                                  "long_end": round(float(t[2] - t[0]) * 0.01, 1),
-                                  "lane_end": round(float(t[3] - t[0]) * 0.01, 1)}
+        if t[0] and t[1] and t[3]:  # microseconds after the first k_sha wave started (an
+            t0 = int(t[0])           # early chain, KNOB_EARLY, starts before it: negative)
+            out["timeline_us"] = {"long_start": round((int(t[1]) - t0) * 0.01, 1),
+                                  "long_end": round((int(t[2]) - t0) * 0.01, 1),
+                                  "lane_end": round((int(t[3]) - t0) * 0.01, 1)}
         if os.environ.get("BSG_DIAG_RAW") == "1":  # experiment builds (BSG_LANE_DIAG)
             out["diag2_raw"] = [int(x) for x in d[8:13]]
         for tag, o in (("long", 3), ("lane", 8)):

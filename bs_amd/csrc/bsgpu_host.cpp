@@ -259,11 +259,16 @@ std::atomic<int64_t>& knob(int k) {
     const char* e = std::getenv("BSG_VERIFY_WINDOW");
     return e ? (int64_t)std::strtoull(e, nullptr, 10) : (int64_t)0;
   }()};
+  static std::atomic<int64_t> early{[] {  // early chains (Early): 1 on, 0 off
+    const char* e = std::getenv("BSG_EARLY");
+    return e ? (int64_t)std::strtoull(e, nullptr, 10) : (int64_t)1;
+  }()};
   static std::atomic<int64_t> none{0};
   switch (k) {
     case BSG_KNOB_SEQ_WAIT: return seq_wait;
     case BSG_KNOB_LONG_MODE: return long_mode;
     case BSG_KNOB_VERIFY_WINDOW: return verify_window;
+    case BSG_KNOB_EARLY: return early;
     default: return none;
   }
 }
@@ -329,6 +334,15 @@ struct bsg_engine {
   bool profile = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float stage_ms[3] = {0, 0, 0};
+  // Early chains (bsgpu_internal.h, Early): the two longest sure chunks hashed on a second
+  // stream from right after k_compact. The Early record lives after the Counters in `ctr`, so
+  // the run's one memset clears both.
+  hipStream_t estream = nullptr;
+  hipEvent_t cand_ev = nullptr, pick_ev = nullptr, early_ev = nullptr;
+  static constexpr uint64_t kEarlyMinBytes = 256ull << 20;  // smaller runs: not worth a stream
+  bool early_ok() const {
+    return !snapshot && !hash_mode && knob(BSG_KNOB_EARLY) != 0;
+  }
 
   void mark(int i) {
     if (profile && ev[i]) (void)hipEventRecord(ev[i], stream);
@@ -380,7 +394,7 @@ struct bsg_engine {
     HCHECK(scount.ensure(sizeof(uint64_t) * (ns ? ns : 1)));
     HCHECK(last_end.ensure(sizeof(uint64_t) * (ns ? ns : 1)));
     HCHECK(carry.ensure(sizeof(CarryOut) * (ns ? ns : 1)));
-    HCHECK(ctr.ensure(sizeof(Counters)));
+    HCHECK(ctr.ensure(sizeof(Counters) + sizeof(Early)));
     HCHECK(long_list.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(order.ensure(sizeof(uint64_t) * (chunk_cap + ns)));
     HCHECK(jinfo.ensure(sizeof(uint32_t) * (chunk_cap + ns)));
@@ -400,9 +414,28 @@ struct bsg_engine {
                           stream));
     HCHECK(hipMemcpyAsync(strip0.p, h_strip0.p, sizeof(uint64_t) * (ns + 1),
                           hipMemcpyHostToDevice, stream));
-    HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
+    HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) + sizeof(Early), stream));
     HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * 2 * kLptBuckets, stream));
     Counters* dctr = ctr.as<Counters>();
+    Early* dearly = reinterpret_cast<Early*>(ctr.as<uint8_t>() + sizeof(Counters));
+    const bool early = early_ok() && total_len >= kEarlyMinBytes && strips;
+    if (early) {
+      if (!estream) HCHECK(stream_acquire(dev, &estream));
+      // device-side dependencies only: no system-scope release (an L2 write-back) at record
+      const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+      if (!cand_ev) HCHECK(hipEventCreateWithFlags(&cand_ev, fl));
+      if (!pick_ev) HCHECK(hipEventCreateWithFlags(&pick_ev, fl));
+      if (!early_ev) HCHECK(hipEventCreateWithFlags(&early_ev, fl));
+    }
+    ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
+               bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
+               carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
+               buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
+               buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
+               jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
+               data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
+               long_mode(), 4u * (uint32_t)num_cus, seq_wait_limit(), cand.as<uint64_t>(),
+               early ? dearly : nullptr};
 
     InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
                 carry.as<CarryOut>()};
@@ -441,7 +474,16 @@ struct bsg_engine {
     HCHECK(dbg("launch_prefix", stream, launch_prefix(pa, stream)));
 
     if (strips) HCHECK(dbg("launch_compact", stream, launch_compact(sa, stream, num_cus)));
-
+    if (early) {  // the sorted candidates are final: pick and start two chains beside selection
+      HCHECK(hipEventRecord(cand_ev, stream));
+      HCHECK(hipStreamWaitEvent(estream, cand_ev, 0));
+      HCHECK(dbg("launch_pick", estream,
+                 launch_pick(cand.as<uint64_t>(), cand_cap, dctr, p.min_size, dearly, estream,
+                             num_cus)));
+      HCHECK(hipEventRecord(pick_ev, estream));
+      HCHECK(dbg("launch_early", estream, launch_early(sh, p.split_bits, estream)));
+      HCHECK(hipEventRecord(early_ev, estream));
+    }
     SelArgs sel{cand.as<uint64_t>(), streams.as<StreamDesc>(), flags.as<uint32_t>(), p, dctr};
     HCHECK(dbg("launch_select", stream, launch_select(sel, cand_cap, stream, num_cus)));
 
@@ -471,17 +513,15 @@ struct bsg_engine {
       HCHECK(hipEventRecord(sel_ev, stream));
     }
 
-    ShaArgs sh{d_data, streams.as<StreamDesc>(), ns, bnd_end.as<uint64_t>(),
-               bnd_info.as<uint64_t>(), last_end.as<uint64_t>(), dctr, out.as<ChunkRec>(),
-               carry.as<CarryOut>(), chunk_cap, long_list.as<uint64_t>(), order.as<uint64_t>(),
-               buckets.as<uint32_t>(), buckets.as<uint32_t>() + kLptBuckets,
-               buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
-               jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
-               data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
-               long_mode(), 4u * (uint32_t)num_cus, seq_wait_limit()};
+    if (early) HCHECK(hipStreamWaitEvent(stream, pick_ev, 0));  // k_lens reads the picks
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
+    if (early) {  // the early chains' records into place, once they are done
+      HCHECK(hipStreamWaitEvent(stream, early_ev, 0));
+      HCHECK(dbg("launch_early_fix", stream, launch_early_fix(dearly, out.as<ChunkRec>(), dctr,
+                                                              stream)));
+    }
     mark(3);
     enqueued = true;
     return BSG_OK;
@@ -1329,13 +1369,14 @@ struct bsg_ctx {
 extern "C" {
 
 int64_t bsg_debug_get(int k) {
-  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_VERIFY_WINDOW) return -1;
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_EARLY) return -1;
   return knob(k).load();
 }
 
 int bsg_debug_set(int k, int64_t value) {
-  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_VERIFY_WINDOW || value < 0) return BSG_EINVAL;
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_EARLY || value < 0) return BSG_EINVAL;
   if (k == BSG_KNOB_LONG_MODE && value > 2) return BSG_EINVAL;
+  if (k == BSG_KNOB_EARLY && value > 1) return BSG_EINVAL;
   knob(k).store(value);
   return BSG_OK;
 }
@@ -1499,6 +1540,13 @@ void bsg_engine_destroy(bsg_engine* e) {
   e->h_ctr.release();
   e->h_snap.release();
   if (e->sel_ev) hipEventDestroy(e->sel_ev);
+  if (e->cand_ev) hipEventDestroy(e->cand_ev);
+  if (e->pick_ev) hipEventDestroy(e->pick_ev);
+  if (e->early_ev) hipEventDestroy(e->early_ev);
+  if (e->estream) {
+    hipStreamSynchronize(e->estream);
+    stream_release(e->dev, e->estream);
+  }
   if (e->stream) stream_release(e->dev, e->stream);
   delete e;
 }

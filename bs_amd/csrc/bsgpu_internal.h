@@ -149,6 +149,23 @@ struct Regions {
                                              // last wave-mode ticket, its start / end, blocks
 };
 
+// Early chains (round 4). A step is bound by its longest chunks' serial SHA-256 chains, and
+// in k_sha they start only after the whole selection (k_select .. k_order, ~0.1-0.3 ms of small
+// dispatches). The sorted candidates already fix the chunks whose both ends are sync points
+// (sure boundaries): on a second stream k_pick takes the kEarly longest of them and k_early
+// hashes them (a helped pair: two chains, two ring fillers) while selection runs; k_lens takes the chunks (same stream, start and end) out of
+// k_sha's queues and k_early_fix writes their records. A pick k_lens does not match is hashed
+// by k_sha as usual.
+constexpr int kEarly = 2;
+struct Early {
+  uint64_t top[kEarly];      // k_pick: (blocks << 32) | i for the chunk (E_i, E_i+1]; 0 = none
+  uint64_t idx[kEarly];      // k_lens: 1 + the chunk's job index (0: not matched)
+  uint64_t diag[5];          // k_early: timing stamps of top[0]'s chain (as Counters::diag)
+  uint64_t pad_;
+  ChunkRec rec[kEarly];      // k_early: the chunks' records
+};
+static_assert(sizeof(Early) % 16 == 0, "Early layout");
+
 constexpr uint32_t kLongMinBlocks = 1024;  // never use the wave path below 64 KiB
 #ifndef BSG_SOLO
 #define BSG_SOLO 16  // configs[2]: the 9th-16th longest jobs on group tickets (1.40 us per

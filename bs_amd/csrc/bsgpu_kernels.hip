@@ -659,6 +659,7 @@ __global__ __launch_bounds__(kScanT) void k_prefix_down(PrefixArgs a) {
 // chunk's start) is >= MinSize is a boundary whatever came before ("sync point"), so the
 // greedy chain restarts there: one lane walks each run of candidates between sync points.
 // ---------------------------------------------------------------------------------------------
+
 __global__ __launch_bounds__(256) void k_select(SelArgs a) {
   if (a.ctr->overflow) return;
   const uint64_t total = a.ctr->ncand;
@@ -1662,6 +1663,19 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
   }
 }
 
+// The chunk k_pick chose for early chain k: its stream and [start, end) (k_lens, k_early).
+__device__ __forceinline__ bool early_key(const ShaArgs& a, int k, uint32_t* s, uint64_t* start,
+                                          uint64_t* end) {
+  const uint64_t top = a.early->top[k];
+  if (!top) return false;
+  const uint64_t c = a.cand[(uint32_t)top], cn = a.cand[(uint32_t)top + 1];
+  *s = cand_stream(c);
+  const uint64_t sb = a.streams[*s].seg_base;
+  *start = sb + cand_pos(c) + 1;
+  *end = sb + cand_pos(cn) + 1;
+  return true;
+}
+
 __global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
   if (a.ctr->overflow || a.ctr->error) return;
   const uint64_t M = a.ctr->nchunks;
@@ -1671,12 +1685,30 @@ __global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
   uint32_t st[8];
   ShaJob jb;
   uint64_t mx = 0, tot = 0;
+  // early chains: the chunks k_early hashes leave k_sha's queues (they still count in the
+  // longest job and the total, so the tiers are those of the whole run)
+  uint32_t es[kEarly] = {~0u, ~0u};
+  uint64_t e0[kEarly] = {0, 0}, e1[kEarly] = {0, 0};
+  if (a.early)
+    for (int k = 0; k < kEarly; ++k)
+      if (!early_key(a, k, &es[k], &e0[k], &e1[k])) es[k] = ~0u;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < njobs; j += stride) {
     uint32_t info = kNoJob;
     if (sha_setup(a, j, M, jb, st)) {
       tot += jb.nblocks;
       // continued chunks (a head from hist) stay per-lane
       if (jb.prefix == 0) mx = max(mx, (uint64_t)jb.nblocks);
+      bool early = false;
+      if (j < M && jb.fin && jb.prefix == 0 && jb.consumed == 0)
+        for (int k = 0; k < kEarly; ++k)
+          if (jb.stream == es[k] && jb.start == e0[k] && jb.end == e1[k]) {
+            a.early->idx[k] = j + 1;
+            early = true;
+          }
+      if (early) {
+        a.jinfo[j] = kNoJob;
+        continue;
+      }
       info = min(jb.nblocks, ~kJobElig) | (jb.prefix == 0 ? kJobElig : 0u);
       LaneJob d;
       d.dptr = reinterpret_cast<uint64_t>(jb.dbase);
@@ -1754,7 +1786,9 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   const bool vb = j0 + cR < jend && sha_setup(a, a.long_list[j0 + cR], M, jb, st);
   const uint32_t nb = vb ? jb.nblocks : 0u;
   uint64_t tm0 = 0, tr0 = 0;
-  if (t == 0) {  // timing stamps of the longest job (read back as Counters::diag)
+  // timing stamps of the longest job (read back as Counters::diag), unless k_early ran it
+  const bool stamp = t == 0 && !(a.early && a.early->top[0]);
+  if (stamp) {
     tm0 = __builtin_amdgcn_s_memtime();
     tr0 = __builtin_amdgcn_s_memrealtime();
   }
@@ -1868,7 +1902,7 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
 #endif
   if (vb && (lane & (B - 1u)) == 0) {
     sha_finish(a, jb, st);
-    if (t == 0) {
+    if (stamp) {
       a.ctr->diag[1] = __builtin_amdgcn_s_memtime();
       a.ctr->diag[3] = __builtin_amdgcn_s_memrealtime();
       a.ctr->diag[0] = tm0;
@@ -1924,20 +1958,12 @@ __device__ bool lds_seq_wait(const ShaArgs& a, uint32_t* p, uint32_t want) {
   return false;
 }
 
-// The chain wave of helped solo ticket t (the workgroup's chain c): sha_wave_job's octet loop
-// over the filler's halves.
-__device__ void sha_solo_chain(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t* lds,
-                               uint32_t c) {
+// The chain wave of a helped solo chain c of the workgroup: sha_wave_job's octet loop over the
+// filler's halves, from the state st of a job of nb blocks. Returns the final state in st (every
+// lane) and false if a handshake timed out (the device error flag is set then).
+__device__ __forceinline__ bool solo_chain_blocks(const ShaArgs& a, uint32_t nb, uint32_t (&st)[8],
+                                                  uint32_t* lds, uint32_t c) {
   const uint32_t lane = threadIdx.x & 63u;
-  ShaJob jb;
-  uint32_t st[8];
-  const bool vb = sha_setup(a, a.long_list[t], M, jb, st);
-  const uint32_t nb = __builtin_amdgcn_readfirstlane(vb ? jb.nblocks : 0u);  // one job: uniform
-  uint64_t tm0 = 0, tr0 = 0;
-  if (t == 0) {  // timing stamps of the longest job (read back as Counters::diag)
-    tm0 = __builtin_amdgcn_s_memtime();
-    tr0 = __builtin_amdgcn_s_memrealtime();
-  }
   const OctLane ol = oct_lane();
   uint32_t hs[4];
   hs[0] = ol.a_side ? st[0] : st[6];
@@ -1950,7 +1976,7 @@ __device__ void sha_solo_chain(const ShaArgs& a, uint64_t M, uint64_t t, uint32_
   uint32_t f = 0;
   for (uint32_t base = 0; base < nb; base += 64, ++f) {
     const uint32_t h = f & 1u;
-    if (!lds_seq_wait(a, fill_seq + h, f / 2 + 1)) return;
+    if (!lds_seq_wait(a, fill_seq + h, f / 2 + 1)) return false;
     const uint32_t* krow = ol.a_side ? ones : lds + (2 * c + h) * kHelpHalfWords;
     const uint32_t stride = ol.a_side ? 0u : 4u * kLongRow;
     sha256_blocks_oct(hs, krow, stride, min(64u, nb - base), (int32_t)nb - (int32_t)base, ol);
@@ -1963,9 +1989,29 @@ __device__ void sha_solo_chain(const ShaArgs& a, uint64_t M, uint64_t t, uint32_
   st[7] = (uint32_t)__shfl((int)hs[1], 0);
   st[4] = (uint32_t)__shfl((int)hs[2], 0);
   st[5] = (uint32_t)__shfl((int)hs[3], 0);
+  return true;
+}
+
+// The chain wave of helped solo ticket t (the workgroup's chain c).
+__device__ void sha_solo_chain(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t* lds,
+                               uint32_t c) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ShaJob jb;
+  uint32_t st[8];
+  const bool vb = sha_setup(a, a.long_list[t], M, jb, st);
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(vb ? jb.nblocks : 0u);  // one job: uniform
+  // timing stamps of the longest job (read back as Counters::diag), unless an early chain
+  // (k_early) ran the longest jobs and stamps them
+  const bool stamp = t == 0 && !(a.early && a.early->top[0]);
+  uint64_t tm0 = 0, tr0 = 0;
+  if (stamp) {
+    tm0 = __builtin_amdgcn_s_memtime();
+    tr0 = __builtin_amdgcn_s_memrealtime();
+  }
+  if (!solo_chain_blocks(a, nb, st, lds, c)) return;
   if (vb && lane == 0) {
     sha_finish(a, jb, st);
-    if (t == 0) {
+    if (stamp) {
       a.ctr->diag[1] = __builtin_amdgcn_s_memtime();
       a.ctr->diag[3] = __builtin_amdgcn_s_memrealtime();
       a.ctr->diag[0] = tm0;
@@ -1975,15 +2021,12 @@ __device__ void sha_solo_chain(const ShaArgs& a, uint64_t M, uint64_t t, uint32_
   }
 }
 
-// The filler wave of helped solo ticket t: fill f is the K+W rows of blocks 64f .. 64f+63
-// (lane l: block 64f + l, the last block again past the end), into half f & 1 once the chain
-// has run that half's previous fill. Each fill's block is requested one fill ahead.
-__device__ void sha_solo_fill(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t* lds,
-                              uint32_t c) {
+// The filler wave of helped solo chain c: fill f is the K+W rows of blocks 64f .. 64f+63 (lane
+// l: block 64f + l, the last block again past the end), into half f & 1 once the chain has run
+// that half's previous fill. Each fill's block is requested one fill ahead.
+__device__ __forceinline__ void solo_fill_blocks(const ShaArgs& a, ShaJob ja, bool va,
+                                                 uint32_t* lds, uint32_t c) {
   const uint32_t lane = threadIdx.x & 63u;
-  ShaJob ja;
-  uint32_t sta[8];
-  const bool va = sha_setup(a, a.long_list[t], M, ja, sta);
   if (!va) {
     ja.dbase = a.data;
     ja.L = 0;
@@ -2031,6 +2074,15 @@ __device__ void sha_solo_fill(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t
     }
     if (lane == 0) lds_seq_store(fill_seq + h, f / 2 + 1);
   }
+}
+
+// The filler wave of helped solo ticket t.
+__device__ void sha_solo_fill(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t* lds,
+                              uint32_t c) {
+  ShaJob ja;
+  uint32_t sta[8];
+  const bool va = sha_setup(a, a.long_list[t], M, ja, sta);
+  solo_fill_blocks(a, ja, va, lds, c);
 }
 
 // The SHA-256 kernel. One 256-thread workgroup per CU (its LDS request admits only one), so
@@ -2112,6 +2164,147 @@ __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
   if ((threadIdx.x & 63u) == 0)
     atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->lane_end_rt),
               (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Early chains (see Early in bsgpu_internal.h).
+// ---------------------------------------------------------------------------------------------
+// k_pick: the two longest chunks (E_i, E_i+1] whose both ends are sure boundaries, i.e. c_i is
+// a sync point (E_i - E_i-1 >= MinSize: k_select makes it a boundary whatever came before) and
+// c_i+1 is one too or is the forced final flush. Chunks below the wave-mode floor are not worth
+// the second stream. Keys are (blocks << 32 | i), so all keys differ.
+__device__ __forceinline__ uint64_t pick_key(const uint64_t* __restrict__ cand, uint64_t n,
+                                             uint64_t i, uint64_t minsz) {
+  if (i == 0 || i + 1 >= n) return 0;
+  const uint64_t c = cand[i];
+  const uint64_t cp = cand[i - 1], cn = cand[i + 1];
+  const uint32_t s = cand_stream(c);
+  if (cand_stream(cp) != s || cand_stream(cn) != s) return 0;
+  const uint64_t E = cand_pos(c) + 1, Ep = cand_pos(cp) + 1, En = cand_pos(cn) + 1;
+  if (E - Ep < minsz) return 0;                        // c_i is not a sync point
+  if (!cand_force(cn) && En - E < minsz) return 0;     // c_i+1 not sure
+  if (cand_force(c)) return 0;                         // (a flush ends its stream)
+  const uint64_t nb = (En - E + 8) / 64 + 1;
+  if (nb < kLongMinBlocks || nb >= (1ull << 31)) return 0;
+  return (nb << 32) | i;
+}
+
+// The two largest of (b1 >= b2) over the wave, in every lane.
+__device__ __forceinline__ void top2_wave(uint64_t& b1, uint64_t& b2) {
+  uint64_t m1 = b1;
+  for (int o = 32; o > 0; o >>= 1) m1 = max(m1, (uint64_t)__shfl_xor((long long)m1, o));
+  uint64_t m2 = b1 == m1 ? b2 : b1;  // the best of all but m1's lane's first
+  for (int o = 32; o > 0; o >>= 1) m2 = max(m2, (uint64_t)__shfl_xor((long long)m2, o));
+  b1 = m1;
+  b2 = m2;
+}
+
+// A small grid (kPickWGs workgroups of 1024 for up to 4 M candidates) reduces to one key pair per workgroup, so top[] sees
+// few atomics (same-address atomics from thousands of waves cost ~0.1 ms). Each workgroup
+// submits its pair: top[0] keeps the maximum, and whatever a submission displaces or loses goes
+// to top[1], which so ends with the largest key other than top[0]'s.
+constexpr uint32_t kPickWGs = 64;
+__global__ __launch_bounds__(1024) void k_pick(const uint64_t* __restrict__ cand, Counters* ctr,
+                                               uint32_t min_size, Early* e) {
+  __shared__ uint64_t wp[2 * 16];
+  if (ctr->overflow || ctr->error) return;
+  const uint64_t n = ctr->ncand;
+  if (n >= (1ull << 32)) return;  // the key carries i in 32 bits
+  uint64_t b1 = 0, b2 = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t key = pick_key(cand, n, i, min_size);
+    b2 = max(b2, min(key, b1));
+    b1 = max(b1, key);
+  }
+  top2_wave(b1, b2);
+  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63u) == 0) {
+    wp[2 * w] = b1;
+    wp[2 * w + 1] = b2;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const uint32_t l = threadIdx.x;
+  b1 = l < 2 * nw ? wp[l] : 0;  // one key per lane: the pairs' members
+  b2 = 0;
+  top2_wave(b1, b2);
+  if (l == 0 && b1) {
+    unsigned long long* t = reinterpret_cast<unsigned long long*>(e->top);
+    const uint64_t old = atomicMax(t, (unsigned long long)b1);
+    if (old < b1) {
+      if (old) atomicMax(t + 1, (unsigned long long)old);
+      if (b2) atomicMax(t + 1, (unsigned long long)b2);
+    } else {
+      atomicMax(t + 1, (unsigned long long)b1);
+    }
+  }
+}
+
+// k_early: one workgroup on the second stream, laid out as a helped solo pair of k_sha<true>:
+// waves 0 and 1 run the chains of the picked chunks 0 and 1, waves 2 and 3 fill their rings.
+__global__ __launch_bounds__(256, 1) void k_early(ShaArgs a, uint32_t split_bits) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  if (a.ctr->overflow || a.ctr->error) return;
+  Early* e = a.early;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kLongRow; i += blockDim.x) lds[kHelpOnes + i] = 1u;
+  if (threadIdx.x < 8) lds[kHelpFlags + threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t c = wv & 1u;
+  ShaJob jb;
+  uint32_t s;
+  if (!early_key(a, (int)c, &s, &jb.start, &jb.end)) return;  // no such pick: the wave leaves
+  const uint64_t cn = a.cand[(uint32_t)e->top[c] + 1];
+  const StreamDesc* sd = a.streams + s;
+  jb.id = c;
+  jb.stream = s;
+  jb.level = cand_tz(cn) >= split_bits ? cand_tz(cn) - split_bits : 0u;
+  jb.fin = 1;
+  jb.prefix = 0;
+  jb.consumed = 0;
+  jb.dbase = a.data + sd->data_off + (jb.start - sd->seg_base);
+  jb.hist = sd->hist + 64;
+  jb.L = jb.end - jb.start;
+  jb.nblocks = (uint32_t)((jb.L + 8) / 64 + 1);
+  __builtin_amdgcn_s_setprio(3);
+  if (wv >= 2) {
+    solo_fill_blocks(a, jb, true, lds, c);
+    return;
+  }
+  uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                    0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  const uint64_t tm0 = __builtin_amdgcn_s_memtime(), tr0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(jb.nblocks);
+  if (!solo_chain_blocks(a, nb, st, lds, c)) return;
+  if (lane == 0) {
+    ChunkRec* r = e->rec + c;
+    r->offset = jb.start;
+    r->len = jb.L;
+    r->level = jb.level;
+    r->stream = jb.stream;
+    uint32_t* ref = reinterpret_cast<uint32_t*>(r->ref);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ref[i] = __builtin_bswap32(st[i]);
+    if (c == 0) {
+      e->diag[1] = __builtin_amdgcn_s_memtime();
+      e->diag[3] = __builtin_amdgcn_s_memrealtime();
+      e->diag[0] = tm0;
+      e->diag[2] = tr0;
+      e->diag[4] = jb.nblocks;
+    }
+  }
+}
+
+// After k_sha and k_early: the early chunks' records into their places (k_lens matched them to
+// their job indices), and the longest one's timing stamps into the counters.
+__global__ void k_early_fix(Early* e, ChunkRec* out, Counters* ctr) {
+  if (ctr->overflow || ctr->error) return;
+  const int k = threadIdx.x;
+  if (k < kEarly && e->top[k] && e->idx[k]) out[e->idx[k] - 1] = e->rec[k];
+  if (k == 0 && e->top[0] && e->idx[0])
+    for (int i = 0; i < 5; ++i) ctr->diag[i] = e->diag[i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2272,6 +2465,25 @@ hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int n
   (void)job_bound;  // persistent: one workgroup per CU, waves loop over the job queues
   hipLaunchKernelGGL(k_sha<true>, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
   hipLaunchKernelGGL(k_sha<false>, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pick(const uint64_t* cand, uint64_t cand_cap, Counters* ctr, uint32_t min_size,
+                       Early* e, hipStream_t s, int num_cus) {
+  // ~64 candidates per thread at most, unless that takes more than 4 workgroups per CU
+  const uint64_t g = std::min<uint64_t>(std::max<uint64_t>(kPickWGs, cand_cap >> 16),
+                                        4ull * (uint32_t)num_cus);
+  hipLaunchKernelGGL(k_pick, dim3((uint32_t)g), dim3(1024), 0, s, cand, ctr, min_size, e);
+  return hipGetLastError();
+}
+
+hipError_t launch_early(const ShaArgs& a, uint32_t split_bits, hipStream_t s) {
+  hipLaunchKernelGGL(k_early, dim3(1), dim3(256), kShaLds, s, a, split_bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_early_fix(Early* e, ChunkRec* out, Counters* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(k_early_fix, dim3(1), dim3(64), 0, s, e, out, ctr);
   return hipGetLastError();
 }
 

@@ -96,6 +96,8 @@ struct ShaArgs {
   uint32_t waves;           // waves of the k_sha grid (4 per CU)
   uint32_t seq_wait_limit;  // polls before a helper-wave handshake flags a device error
                             // (~1 s; BSG_DEBUG_SEQ_WAIT overrides it, 0: fail at once, tests)
+  const uint64_t* cand;     // early chains: the sorted candidates (k_lens decodes the picks)
+  Early* early;             // early chains of this run, or nullptr
 };
 
 struct BlobShaArgs {
@@ -120,6 +122,12 @@ hipError_t launch_blob_jobs(const ChunkArgs& a, const StreamDesc* streams, uint3
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_longlist(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);
 hipError_t launch_sha_blobs(const BlobShaArgs& a, hipStream_t s, int num_cus);
+// Early chains (see Early): picked and hashed on a second stream from k_compact on (k_lens waits
+// for the picks), the records' fix-up on the engine stream after k_sha (it waits for the chains).
+hipError_t launch_pick(const uint64_t* cand, uint64_t cand_cap, Counters* ctr, uint32_t min_size,
+                       Early* e, hipStream_t s, int num_cus);
+hipError_t launch_early(const ShaArgs& a, uint32_t split_bits, hipStream_t s);
+hipError_t launch_early_fix(Early* e, ChunkRec* out, Counters* ctr, hipStream_t s);
 // Device -> pinned host bytes by a kernel on stream s (dst: the device alias of a hipHostMalloc
 // buffer). Unlike hipMemcpyAsync D2H, a kernel waiting in its own stream for the work before
 // it holds no place in the shared copy-engine queue, so it cannot stall other streams' H2D.

@@ -141,7 +141,9 @@ void bsg_engine_destroy(bsg_engine* eng);
 /* Enqueue split + hash of nstreams streams d_data[off[i] .. off[i]+len[i]) (device memory,
  * off[i] % 16 == 0; off/len are host arrays; at most 65,535 streams of < 2^40 bytes each, a
  * device-memory bound: one stream of a run lies whole in device memory).
- * Asynchronous on the engine's stream.
+ * Asynchronous on the engine's stream (a run of >= 256 MiB hashes its two longest chunks on a
+ * second pooled stream, which the engine's stream waits for before the run completes; see
+ * BSG_KNOB_EARLY).
  * The allocation holding d_data must extend at least BSG_READ_SLACK bytes past the end of the
  * last stream (the SHA-256 loader reads whole 64-byte blocks and masks the excess). */
 #define BSG_READ_SLACK 256
@@ -294,6 +296,9 @@ void bsg_reader_free(bsg_reader* r);
 #define BSG_KNOB_LONG_MODE 2     /* BSG_LONG_MODE: wave-mode tiers 0 auto, 1 off, 2 all */
 #define BSG_KNOB_VERIFY_WINDOW 3 /* BSG_VERIFY_WINDOW: split::Reader verify window in bytes
                                   * (0: 256 MiB), read when a Reader is opened */
+#define BSG_KNOB_EARLY 4         /* BSG_EARLY: 1 (default) hashes the two longest chunks whose
+                                  * ends are sure boundaries on a second stream from right after
+                                  * candidate compaction (engine runs of >= 256 MiB); 0 off */
 int bsg_debug_set(int knob, int64_t value);
 int64_t bsg_debug_get(int knob); /* -1 for an unknown knob */
 

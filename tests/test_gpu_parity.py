@@ -309,6 +309,41 @@ def test_engine_1gib_full_parity(gpu, oracle, table):
     eng.close()
 
 
+def test_early_chains_on_off(gpu, oracle, table):
+    """Early chains (KNOB_EARLY): the two longest chunks whose ends are sure
+    boundaries are hashed on a second stream from right after k_compact. Stream 0 is cut one
+    byte before the end of its longest chunk, so its final (forced) chunk is the run's longest
+    and early slot 0 takes it; slot 1 takes an ordinary chunk. Records with the knob on and off
+    and the oracle's are identical, and the longest chain's stamps come from the early chain
+    (it starts before k_sha does: a negative long_start)."""
+    from bs_amd.synth import splitmix_array
+    seed = 0xE4C2  # its longest chunk (658,353 B) ends at 263 MiB: the run is >= 256 MiB
+    full = splitmix_array(seed, 270 << 20)
+    one = oracle.split(table, full)
+    k = int(np.argmax(one["len"][:-1]))
+    n0 = int(one["offset"][k] + one["len"][k]) - 1
+    lens = [n0, 40 << 20]
+    assert sum(lens) >= 256 << 20  # engine runs below that take no early chains
+    want = [oracle.split(table, full[:n0]), oracle.split(table, splitmix_array(seed + 1, lens[1]))]
+    assert int(want[0]["len"][-1]) == int(one["len"][k]) - 1
+    got = {}
+    for on in (1, 0):
+        with gpu.debug_knob(gpu.KNOB_EARLY, on):
+            eng, buf, offs = _device_stream_run(gpu, lens, seed)
+            got[on] = (as_tuples(eng.chunks()), [int(c) for c in eng.counts()], eng.diag())
+            eng.close()
+            buf.free()
+    assert got[1][:2] == got[0][:2]
+    ch, counts = got[1][0], got[1][1]
+    assert counts == [len(w) for w in want]
+    assert ch == as_tuples(want[0]) + as_tuples(want[1])
+    tl = got[1][2].get("timeline_us")
+    assert tl and tl["long_start"] < 0, got[1][2]
+    assert got[1][2]["long"]["blocks"] == (int(one["len"][k]) - 1 + 8) // 64 + 1
+    tl0 = got[0][2].get("timeline_us")
+    assert tl0 and tl0["long_start"] >= 0, got[0][2]
+
+
 def test_dedup_edited_streams(gpu, oracle, table):
     """BASELINE config 5 (dedup), scaled to 2 x 64 MiB: stream B = stream A with 1 % seeded
     edits (64 sites x 10486 B). Both streams split in one batch must equal the oracle, and the
