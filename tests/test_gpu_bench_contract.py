@@ -59,7 +59,7 @@ def test_bench_default_carries_configs2():
     c2 = d["configs2"]
     assert c2["workload"].startswith("configs[2]") and c2["steps"] == 1
     assert c2["value"] > d["value"] and c2["ms_per_step"] > 0
-    assert c2["roofline"]["kernel"] == "k_sha" and c2["roofline"]["frac"] > 0
+    assert c2["roofline"]["kernel"].startswith("k_sha") and c2["roofline"]["frac"] > 0
     assert c2["roofline"]["k_scan"]["frac"] > 0
     assert c2["cpu_baseline"]["cores"] >= 1 and c2["cpu_baseline"]["full_writer"]["value"] > 0
     assert set(c2["stage_ms"]) == set(d["stage_ms"])
