@@ -339,6 +339,7 @@ struct bsg_engine {
   // the run's one memset clears both.
   hipStream_t estream = nullptr;
   hipEvent_t cand_ev = nullptr, pick_ev = nullptr, early_ev = nullptr;
+  bool early_open = false;  // chains launched whose end the engine stream does not wait for yet
   static constexpr uint64_t kEarlyMinBytes = 256ull << 20;  // smaller runs: not worth a stream
   bool early_ok() const {
     return !snapshot && !hash_mode && knob(BSG_KNOB_EARLY) != 0;
@@ -352,6 +353,10 @@ struct bsg_engine {
 
   int enqueue() {
     const uint32_t ns = nstreams;
+    if (early_open) {  // a failed run left early chains its engine stream never waited for
+      HCHECK(hipEventSynchronize(early_ev));
+      early_open = false;
+    }
     // strips
     std::vector<uint64_t> s0(ns + 1);
     uint64_t strips = 0, total_len = 0, chunk_bound = 0;
@@ -483,6 +488,7 @@ struct bsg_engine {
       HCHECK(hipEventRecord(pick_ev, estream));
       HCHECK(dbg("launch_early", estream, launch_early(sh, p.split_bits, estream)));
       HCHECK(hipEventRecord(early_ev, estream));
+      early_open = true;
     }
     SelArgs sel{cand.as<uint64_t>(), streams.as<StreamDesc>(), flags.as<uint32_t>(), p, dctr};
     HCHECK(dbg("launch_select", stream, launch_select(sel, cand_cap, stream, num_cus)));
@@ -519,6 +525,7 @@ struct bsg_engine {
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
     if (early) {  // the early chains' records into place, once they are done
       HCHECK(hipStreamWaitEvent(stream, early_ev, 0));
+      early_open = false;  // the engine stream now orders everything after the chains
       HCHECK(dbg("launch_early_fix", stream, launch_early_fix(dearly, out.as<ChunkRec>(), dctr,
                                                               stream)));
     }
