@@ -27,6 +27,7 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FETCH_X2 = {"bsg::k_sha(bsg::ShaArgs)", "void bsg::k_sha<true>(bsg::ShaArgs)",
             "void bsg::k_sha<false>(bsg::ShaArgs)", "bsg::k_sha_blobs(bsg::BlobShaArgs)",
+            "bsg::k_early(bsg::ShaArgs, unsigned int)",
             "void bsg::k_scan<true>(bsg::ScanArgs)", "void bsg::k_scan<false>(bsg::ScanArgs)",
             "bsg::k_refine(bsg::ScanArgs)"}
 STRIP_PATTERN = {"void bsg::k_scan<true>(bsg::ScanArgs)", "void bsg::k_scan<false>(bsg::ScanArgs)"}
