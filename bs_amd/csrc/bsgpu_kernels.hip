@@ -97,13 +97,20 @@ __device__ __forceinline__ uint32_t lookup(const uint32_t* tab, uint32_t w, uint
   return lds_u32(tab, tab_addr(w, lane4, k));
 }
 
+// Called by kScanWG-thread workgroups only (k_scan, k_refine, k_rescan). 256 rows x 64 replicas;
+// each uint4 store writes 4 replicas of one row. A thread issues all of its loads before its
+// stores: as a load-store loop, each of the 8 iterations waited for its global load (~8
+// dependent L2 round trips at the start of every workgroup, before any scanning).
 __device__ __forceinline__ void load_table(uint32_t* tab, const uint32_t* __restrict__ T) {
-  // 256 rows x 64 replicas; each uint4 store writes 4 replicas of one row.
+  constexpr uint32_t kVec = kTabRows * kTabRep / 4;
+  constexpr uint32_t kPer = kVec / kScanWG;
+  static_assert(kVec % kScanWG == 0, "table stores per thread");
   u32x4a* t4 = reinterpret_cast<u32x4a*>(tab);
-  for (uint32_t i = threadIdx.x; i < kTabRows * kTabRep / 4; i += blockDim.x) {
-    uint32_t v = T[i >> 4];
-    t4[i] = u32x4a{v, v, v, v};
-  }
+  uint32_t v[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) v[k] = T[(threadIdx.x + k * kScanWG) >> 4];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) t4[threadIdx.x + k * kScanWG] = u32x4a{v[k], v[k], v[k], v[k]};
 }
 
 template <class P>
