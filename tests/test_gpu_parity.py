@@ -344,6 +344,47 @@ def test_early_chains_on_off(gpu, oracle, table):
     assert tl0 and tl0["long_start"] >= 0, got[0][2]
 
 
+def test_early_chains_concurrent_engines(gpu, oracle, table):
+    """Three engines on three host threads, each running a >= 256 MiB batch with early chains at
+    the same time (six HIP streams over the process's hardware queues, cross-stream waits in
+    both directions), twice: every run's records equal that engine's run alone with the early
+    chains off, and stream 0 of the first engine equals the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    from bs_amd.synth import splitmix_array
+    lens = [[200 << 20, 60 << 20 | 12345], [270 << 20], [130 << 20, 130 << 20, 1 << 20]]
+    seeds = [0xC0C0, 0xC1C1, 0xC2C2]
+
+    def prepare(k):
+        offs, total = [], 0
+        for n in lens[k]:
+            offs.append(total)
+            total += (n + 15) & ~15
+        buf = gpu.DeviceBuffer(total + 4096)
+        eng = gpu.Engine()
+        for i, (o, n) in enumerate(zip(offs, lens[k])):
+            gpu.fill_splitmix(buf.ptr + o, n, seeds[k] + i, stream=eng.stream)
+        return eng, buf, offs
+
+    def run(k, eng, buf, offs):
+        eng.run(buf.ptr, offs, lens[k], bits=16, min_size=1024)
+        eng.finish()
+        return as_tuples(eng.chunks()), [int(c) for c in eng.counts()]
+
+    setups = [prepare(k) for k in range(3)]
+    with gpu.debug_knob(gpu.KNOB_EARLY, 0):
+        alone = [run(k, *setups[k]) for k in range(3)]
+    with gpu.debug_knob(gpu.KNOB_EARLY, 1):
+        with ThreadPoolExecutor(3) as ex:
+            for _ in range(2):
+                got = list(ex.map(lambda k: run(k, *setups[k]), range(3)))
+                assert got == alone
+    want0 = as_tuples(oracle.split(table, splitmix_array(seeds[0], lens[0][0])))
+    assert alone[0][0][:alone[0][1][0]] == want0
+    for eng, buf, _ in setups:
+        eng.close()
+        buf.free()
+
+
 def test_dedup_edited_streams(gpu, oracle, table):
     """BASELINE config 5 (dedup), scaled to 2 x 64 MiB: stream B = stream A with 1 % seeded
     edits (64 sites x 10486 B). Both streams split in one batch must equal the oracle, and the
