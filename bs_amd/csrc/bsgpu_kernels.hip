@@ -1077,11 +1077,12 @@ __device__ uint32_t pick_region(const ShaArgs& a, uint32_t R, uint32_t start) {
 #define BSG_REGION_POLL 8      // a wave compares its region's progress with the others' every
 #endif                         // this many pops (0: only when its region runs dry)
 #ifndef BSG_REGION_LAG
-#define BSG_REGION_LAG 3       // ... and moves if it is this many % of its jobs ahead of the
-#endif                         // region furthest behind
+#define BSG_REGION_LAG 3       // BSG_REGION_BY_LEN=0 only: ... and moves if it is this many % of
+#endif                         // its jobs ahead of the region furthest behind
 
-// Regions are drained longest job first, so the share of a region's jobs already taken says how
-// far down its length order it is. Returns the region furthest behind if `cur` is more than
+// (Round-2 poll, kept for BSG_REGION_BY_LEN=0.) Regions are drained longest job first, so the
+// share of a region's jobs already taken says how far down its length order it is (but not how
+// long its next job is). Returns the region furthest behind if `cur` is more than
 // BSG_REGION_LAG % ahead of it, else `cur`. One round of loads; called by a whole wave.
 __device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
   const uint64_t act = __ballot(1);
@@ -1117,6 +1118,55 @@ __device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
   if (!best) return cur;
   const uint32_t behind_taken = (1u << 20) - (uint32_t)(best >> 8);
   if (cur_taken <= behind_taken + (uint32_t)(((1ull << 20) * BSG_REGION_LAG) / 100)) return cur;
+  return (cur + 255u - (uint32_t)(best & 255u)) % R;
+}
+
+#ifndef BSG_REGION_BY_LEN
+#define BSG_REGION_BY_LEN 1    // poll by next-job length (0: by share taken, behind_region)
+#endif
+#ifndef BSG_REGION_LEN_LAG
+#define BSG_REGION_LEN_LAG 25  // ... moving if another region's next job is this many % longer
+#endif
+// The region whose next job is the longest, if that job is more than BSG_REGION_LEN_LAG % longer
+// than `cur`'s next one, else `cur`. Regions are drained longest first, so this keeps the waves
+// close to one global longest-first order, and the per-lane waves end together: on configs[2]
+// the poll by share taken let them end over ~0.35 ms, the last ones ~0.18 ms after the longest
+// chain; by length they end with it (+1 %, profiles/r04_region_len_ab.log).
+__device__ uint32_t longer_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
+  const uint64_t act = __ballot(1);
+  const uint32_t nact = (uint32_t)__popcll(act);
+  const uint32_t rank =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  uint64_t key = 0;   // next job's blocks << 8 | (255 - distance from cur)
+  uint32_t mine = 0;  // cur's next job's blocks (0: dry), on the lane that read it
+  bool has_mine = false;
+  for (uint32_t r = rank; r < R; r += nact) {
+    const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
+    const uint64_t h = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t len = 0;
+    if (h < n) len = (a.jinfo[a.rorder[o + h]] & ~kJobElig) + 1u;
+    if (r == cur) {
+      mine = len;
+      has_mine = true;
+    }
+    if (len) {
+      const uint64_t k = ((uint64_t)len << 8) | (255u - (r + R - cur) % R);
+      key = k > key ? k : key;
+    }
+  }
+  uint64_t best = 0;
+  uint32_t cur_len = 0;
+  for (uint64_t m = act; m; m &= m - 1) {
+    const int l = (int)__builtin_ctzll(m);
+    const uint64_t v =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), l) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, l);
+    best = v > best ? v : best;
+    if (__builtin_amdgcn_readlane((int)has_mine, l)) cur_len = (uint32_t)__builtin_amdgcn_readlane((int)mine, l);
+  }
+  if (!best) return cur;
+  const uint64_t best_len = best >> 8;
+  if (best_len * 100 <= (uint64_t)cur_len * (100 + BSG_REGION_LEN_LAG)) return cur;
   return (cur + 255u - (uint32_t)(best & 255u)) % R;
 }
 
@@ -1224,7 +1274,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
     if (BSG_REGION_POLL && poll && !all_done && R > 1) {
       // keep the regions level: move to the one furthest behind if this one is well ahead
       poll = false;
-      const uint32_t r2 = behind_region(a, R, reg);
+      const uint32_t r2 = BSG_REGION_BY_LEN ? longer_region(a, R, reg) : behind_region(a, R, reg);
       if (r2 != reg) {
         reg = r2;
         reg_off = a.reg->off[reg];
