@@ -156,8 +156,12 @@ __device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t st
 // those bytes), then each position gets the exact test tz >= bits (equivalent to the fast
 // pass's mask test for bits <= 32; Bits > 32 never splits, hashsplit's tz >= SplitBits with
 // tz <= 32). Loads are whole 64-byte blocks (BSG_READ_SLACK makes the tail block readable).
-// Returns the hash at the last position scanned.
-template <bool WRITE>
+// Returns the hash at the last position scanned. FULL (n == 64, every hit block): the lookups of
+// each group of kExactGroup positions are issued together before its steps; with a per-position
+// `k < n` test every step was its own basic block and waited for its own two LDS reads (k_refine
+// ~26 us on 16 K strips).
+constexpr int kExactGroup = 8;
+template <bool WRITE, bool FULL>
 __device__ __forceinline__ uint32_t exact_block(const ScanArgs& a, const uint32_t* tab,
                                                 uint32_t lane4, const uint8_t* blk,
                                                 const uint8_t* prev, uint32_t n, StripCtx& c,
@@ -169,14 +173,32 @@ __device__ __forceinline__ uint32_t exact_block(const ScanArgs& a, const uint32_
 #pragma unroll
   for (int k = 0; k < 64; ++k) h = rotl1(h) ^ lookup(tab, pw[k >> 2], lane4, k);
   const uint32_t bits = a.p.split_bits;
+  if constexpr (FULL) {
 #pragma unroll
-  for (int k = 0; k < 64; ++k) {
-    if ((uint32_t)k < n) {
-      const uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
-      const uint32_t tout = lookup(tab, pw[k >> 2], lane4, k);
-      h = xor3(rotl1(h), tout, tin);
-      const uint32_t tz = tz32(h);
-      if (tz >= bits) emit<WRITE>(a, c, strip, off + k, false, tz);
+    for (int q = 0; q < 64; q += kExactGroup) {
+      uint32_t tin[kExactGroup], tout[kExactGroup];
+#pragma unroll
+      for (int k = 0; k < kExactGroup; ++k) {
+        tin[k] = lookup(tab, w[(q + k) >> 2], lane4, q + k);
+        tout[k] = lookup(tab, pw[(q + k) >> 2], lane4, q + k);
+      }
+#pragma unroll
+      for (int k = 0; k < kExactGroup; ++k) {
+        h = xor3(rotl1(h), tout[k], tin[k]);
+        const uint32_t tz = tz32(h);
+        if (tz >= bits) emit<WRITE>(a, c, strip, off + q + k, false, tz);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      if ((uint32_t)k < n) {
+        const uint32_t tin = lookup(tab, w[k >> 2], lane4, k);
+        const uint32_t tout = lookup(tab, pw[k >> 2], lane4, k);
+        h = xor3(rotl1(h), tout, tin);
+        const uint32_t tz = tz32(h);
+        if (tz >= bits) emit<WRITE>(a, c, strip, off + k, false, tz);
+      }
     }
   }
   return h;
@@ -440,7 +462,7 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
   while (hits) {
     const uint64_t off = l.start + 64ull * (uint32_t)__builtin_ctz(hits);
     hits &= hits - 1;
-    exact_block<WRITE>(a, tab, lane4, d + off, off >= 64 ? d + off - 64 : sd->hist, 64u, c,
+    exact_block<WRITE, true>(a, tab, lane4, d + off, off >= 64 ? d + off - 64 : sd->hist, 64u, c,
                        strip, off);
   }
   const uint32_t rem = l.len & 63u;
@@ -449,7 +471,7 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
     // the hash entering the tail (or, with no tail, at the segment's last byte) is rebuilt
     // from the 64 bytes before the tail's 64-aligned start
     const uint64_t off = l.start + (l.len & ~63u);
-    const uint32_t h = exact_block<WRITE>(a, tab, lane4, d + off,
+    const uint32_t h = exact_block<WRITE, false>(a, tab, lane4, d + off,
                                           off >= 64 ? d + off - 64 : sd->hist, rem, c, strip, off);
     if (flush) emit<WRITE>(a, c, strip, l.start + l.len - 1, true, tz32(h));
   }
@@ -488,7 +510,8 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
 // default Bits 16; all of them on degenerate data), one per lane from the compacted list, so
 // the waves are full: exact counts into counts[], the first kSlotCap candidates into the
 // strip's slots; strips with more are left to k_rescan.
-__global__ __launch_bounds__(kScanWG, 2) void k_refine(ScanArgs a) {
+// 4 waves per SIMD (<= 128 VGPRs): two workgroups per CU, as its LDS allows
+__global__ __launch_bounds__(kScanWG, 4) void k_refine(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
   if (!table_at_lds0(tab)) {
     if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
