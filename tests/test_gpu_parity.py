@@ -344,6 +344,32 @@ def test_early_chains_on_off(gpu, oracle, table):
     assert tl0 and tl0["long_start"] >= 0, got[0][2]
 
 
+@pytest.mark.parametrize("bits,min_size", [(13, 8192), (20, 64), (16, 65536), (14, 1)])
+def test_early_chains_params(gpu, oracle, table, bits, min_size):
+    """The sure-boundary rule behind the early picks (E_i - E_i-1 >= MinSize) under other
+    params: a large MinSize (few sync points, long forced walks), tiny MinSize, 1 MiB chunks.
+    A 260 MiB stream plus a short one; records with the early chains on and off and the
+    oracle's identical."""
+    from bs_amd.synth import splitmix_array
+    lens = [260 << 20, 3 << 20]
+    seed = 0xEA00 + bits
+    got, tl = {}, {}
+    for on in (1, 0):
+        with gpu.debug_knob(gpu.KNOB_EARLY, on):
+            eng, buf, offs = _device_stream_run(gpu, lens, seed, bits=bits, min_size=min_size)
+            got[on] = (as_tuples(eng.chunks()), [int(c) for c in eng.counts()])
+            tl[on] = eng.diag().get("timeline_us", {})
+            eng.close()
+            buf.free()
+    assert got[1] == got[0]
+    assert tl[1]["long_start"] < 0 <= tl[0]["long_start"], tl  # the longest ran early
+    want = []
+    for i, n in enumerate(lens):
+        want += as_tuples(oracle.split(table, splitmix_array(seed + i, n), bits=bits,
+                                       min_size=min_size))
+    assert got[1][0] == want
+
+
 def test_early_chains_concurrent_engines(gpu, oracle, table):
     """Three engines on three host threads, each running a >= 256 MiB batch with early chains at
     the same time (six HIP streams over the process's hardware queues, cross-stream waits in
