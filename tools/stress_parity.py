@@ -3,7 +3,10 @@ splits and (round 3) C++ split.Writer runs with small and large Writes mixed, ag
 oracle. python tools/stress_parity.py [N] [seed_base] -- prints a line per 20 draws.
 STRESS_WRITER=0 restores the round-1/2 mix (batch and streaming draws only). Round 4: a third of
 the streaming and Writer draws start their stream at a random offset past 2^40
-(bsg_set_stream_base): streaming records must be the oracle's shifted by it, Writer Roots equal."""
+(bsg_set_stream_base): streaming records must be the oracle's shifted by it, Writer Roots equal;
+every 10th draw is instead a device-resident engine run of 256-320 MiB over 1-6 streams, the
+size at which the early chains (BSG_KNOB_EARLY) take the longest sure chunks to a second stream
+(STRESS_ENGINE=0 leaves them out)."""
 import os
 import sys
 import time
@@ -33,7 +36,36 @@ def main():
             bits = int(rng.choice([4, 6, 8, 12, 33, 40]))
             mn = int(rng.choice([1, 17, 63, 64]))
         kind = d % 3 if os.environ.get("STRESS_WRITER", "1") == "1" else d % 2
-        if kind == 2:  # the C++ split.Writer: Writes of 1 KB to 9 MiB mixed, tiles 64 KiB-256 MiB
+        if d % 10 == 9 and os.environ.get("STRESS_ENGINE", "1") == "1":
+            kind = 3
+        if kind == 3:  # device-resident engine run >= 256 MiB: early chains beside selection
+            bits = int(rng.integers(10, 23))  # (records the Python comparison can hold)
+            mn = int(rng.choice([64, 512, 1024, 4096, 65536]))
+            ns = int(rng.integers(1, 7))
+            total = int(rng.integers(256 << 20, 320 << 20))
+            cuts = np.sort(rng.integers(0, total, size=ns - 1))
+            lens = [int(x) for x in np.diff(np.concatenate([[0], cuts, [total]]))]
+            offs, span = [], 0
+            for n in lens:
+                offs.append(span)
+                span += (n + 15) & ~15
+            buf = bsgpu.DeviceBuffer(span + 4096)
+            eng = bsgpu.Engine()
+            seed0 = 4_000_000 + 97 * d
+            for i, (o, n) in enumerate(zip(offs, lens)):
+                bsgpu.fill_splitmix(buf.ptr + o, n, seed0 + i, stream=eng.stream)
+            eng.run(buf.ptr, offs, lens, bits=bits, min_size=mn)
+            eng.finish()
+            ch, counts = eng.chunks(), eng.counts()
+            k = 0
+            for i, n in enumerate(lens):
+                want = tuples(O.split(table, splitmix_array(seed0 + i, n), bits=bits, min_size=mn))
+                got = tuples(ch[k:k + int(counts[i])])
+                assert got == want, ("engine", d, i, bits, mn, lens)
+                k += int(counts[i])
+            eng.close()
+            buf.free()
+        elif kind == 2:  # the C++ split.Writer: Writes of 1 KB to 9 MiB mixed, tiles 64 KiB-256 MiB
             n = int(rng.integers(0, 40_000_000))
             data = splitmix_array(3_000_000 + d, n)
             tile = int(rng.choice([65536, 1 << 20, 5 << 20, 16 << 20, 256 << 20]))
