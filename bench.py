@@ -302,6 +302,9 @@ def pmc_traffic(kernel: str, workload: str):
 CONFIGS1 = "configs[1]: 1 GiB random stream per GPU, default split params"
 CONFIGS2 = "configs[2]: 256 x 64 MiB streams per GPU"
 STAGES = ["k_scan", "k_compact+k_select+k_chunks+prefix", "k_sha"]
+STAGE_SRC = ("HIP events on the engine's stream: k_sha (the roofline's kernel) over the timed "
+             "steps; k_scan and selection over the warmup steps after the first (their two "
+             "extra events per step are left out of the timed region)")
 
 
 def workload_name(ns: int, nbytes: int, bits: int, min_size: int) -> str:
@@ -321,33 +324,41 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
     stride = (nbytes + 15) & ~15
     buf = bsgpu.DeviceBuffer(stride * ns, device=local)
     eng = bsgpu.Engine(device=local)
-    eng.profile(True)
     offs = [i * stride for i in range(ns)]
     lens = [nbytes] * ns
     for i in range(ns):  # stream s of rank r uses seed BASE + r*ns + s
         bsgpu.fill_splitmix(buf.ptr + offs[i], nbytes, BASE_SEED + rank * ns + i,
                             stream=eng.stream, device=local)
+    # Stage times come from HIP events on the engine's stream, and every event costs the step
+    # time (≈ 0.05 ms for four on configs[1], tools/profile_cost.py): the warmup steps time all
+    # three stages, the timed steps only the SHA-256 stage (the dominant kernel, two events).
     stage_sum = [0.0, 0.0, 0.0]
-    nsteps = [0]
+    nsteps = [0, 0]  # warmup steps with all stages timed (the first, cold, left out), timed steps
 
-    def step():
+    def step(warm=False):
         eng.run(buf.ptr, offs, lens, bits=bits, min_size=min_size)
         eng.finish()  # waits on the engine's stream; records stay in HBM
         ms = eng.stage_ms()
-        for i in range(3):
-            stage_sum[i] += ms[i]
-        nsteps[0] += 1
+        if warm:
+            for i in range(2):
+                stage_sum[i] += ms[i]
+            nsteps[0] += 1
+        else:
+            stage_sum[2] += ms[2]
+            nsteps[1] += 1
 
     def sync():
         bsgpu.synchronize(local)
 
-    # warmup steps are counted into stage_sum too; reset after them
-    for _ in range(warmup):
-        step()
-    stage_sum[:] = [0.0, 0.0, 0.0]
-    nsteps[0] = 0
+    eng.profile(1)
+    for w in range(warmup):
+        step(warm=w > 0 or warmup == 1)
+    eng.profile(2)
     elapsed = timed_steps(step, sync, world, steps, 0)
-    stage_avg = [s / max(nsteps[0], 1) for s in stage_sum]
+    stage_avg = [stage_sum[0] / max(nsteps[0], 1), stage_sum[1] / max(nsteps[0], 1),
+                 stage_sum[2] / max(nsteps[1], 1)]
+    if nsteps[0] == 0:  # no warmup: the scan and selection stages were not timed
+        stage_avg[0] = stage_avg[1] = 0.0
     diag = eng.diag()
     chunks = int(eng.nchunks)
     # the last timed step's records, copied to the host after timing: checked below against
@@ -474,6 +485,7 @@ def main():
               "unit": "GiB/s", "steps": args.configs2_steps, "warmup": args.warmup,
               "ms_per_step": round(leg2["elapsed"] * 1e3 / args.configs2_steps, 3),
               "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, leg2["stage_avg"])},
+              "stage_ms_src": STAGE_SRC,
               "chunks_per_step": leg2["chunks"],
               "roofline": roofline(CONFIGS2, ns2 * n2, leg2["stage_avg"]),
               "cpu_baseline": leg2["cpu"], "sha_path": leg2["diag"],
@@ -509,6 +521,7 @@ def main():
             "cpu_baseline": leg["cpu"],
             "end_to_end": e2e,
             "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, stage_avg)},
+            "stage_ms_src": STAGE_SRC,
             "chunks_per_step": leg["chunks"],
             "sha_path": leg["diag"],
             "chain_roofline": chain_roofline(leg["diag"]),

@@ -419,7 +419,8 @@ class Engine:
     def stream(self) -> int:
         return lib().bsg_engine_stream(self.h) or 0
 
-    def profile(self, enable: bool = True) -> None:
+    def profile(self, enable: int = 1) -> None:
+        """bsg_engine_profile: 0 off, 1 (or True) every stage, 2 the SHA-256 stage only."""
         _check(lib().bsg_engine_profile(self.h, int(enable)), "bsg_engine_profile")
 
     def stage_ms(self) -> list[float]:

@@ -331,7 +331,7 @@ struct bsg_engine {
   bool hash_mode = false;  // bsg_engine_hash: every stream is one blob (enqueue_hash)
   Counters last{};
   // optional per-stage HIP events on the engine stream: [scan, compact..chunks, sha]
-  bool profile = false;
+  int profile = 0;  // bsg_engine_profile mode
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float stage_ms[3] = {0, 0, 0};
   // Early chains (bsgpu_internal.h, Early): the two longest sure chunks hashed on a second
@@ -345,8 +345,8 @@ struct bsg_engine {
     return !snapshot && !hash_mode && knob(BSG_KNOB_EARLY) != 0;
   }
 
-  void mark(int i) {
-    if (profile && ev[i]) (void)hipEventRecord(ev[i], stream);
+  void mark(int i) {  // profile 1: every stage boundary; 2: the SHA-256 stage's two only
+    if (profile && ev[i] && (profile == 1 || i >= 2)) (void)hipEventRecord(ev[i], stream);
   }
 
   int setdev() { return herr(hipSetDevice(dev)); }
@@ -617,7 +617,8 @@ struct bsg_engine {
     enqueued = false;
     if (profile) {
       for (int i = 0; i < 3; ++i)
-        if (hipEventElapsedTime(&stage_ms[i], ev[i], ev[i + 1]) != hipSuccess) {
+        if ((profile == 2 && i < 2) ||
+            hipEventElapsedTime(&stage_ms[i], ev[i], ev[i + 1]) != hipSuccess) {
           (void)hipGetLastError();
           stage_ms[i] = -1.f;
         }
@@ -1654,12 +1655,12 @@ int bsg_engine_copy_counts(bsg_engine* e, uint64_t* counts, uint32_t nstreams) {
 void* bsg_engine_stream(bsg_engine* e) { return e ? (void*)e->stream : nullptr; }
 
 int bsg_engine_profile(bsg_engine* e, int enable) {
-  if (!e) return BSG_EINVAL;
+  if (!e || enable < 0 || enable > 2) return BSG_EINVAL;
   int rc = e->setdev();
   if (rc) return rc;
   if (enable && !e->ev[0])
     for (int i = 0; i < 4; ++i) HCHECK(hipEventCreate(&e->ev[i]));
-  e->profile = enable != 0;
+  e->profile = enable;
   return BSG_OK;
 }
 

@@ -167,9 +167,11 @@ int bsg_engine_copy_chunks(bsg_engine* eng, bsg_chunk* out, uint64_t cap);
 int bsg_engine_copy_counts(bsg_engine* eng, uint64_t* counts, uint32_t nstreams);
 /* The engine's HIP stream (hipStream_t), e.g. for event timing. */
 void* bsg_engine_stream(bsg_engine* eng);
-/* Per-stage HIP event timing of later runs (enable != 0), and the last finished run's stage
- * durations in ms: [0] rolling scan (k_scan), [1] prefix/compact/select/chunks, [2] SHA-256
- * (k_sha). Timed on the engine's own stream. */
+/* Per-stage HIP event timing of later runs, and the last finished run's stage durations in
+ * ms: [0] rolling scan (k_scan), [1] prefix/compact/select/chunks, [2] SHA-256 (k_sha, and the
+ * early chains' tail). Timed on the engine's own stream. enable: 0 off, 1 every stage (four
+ * events per run), 2 the SHA-256 stage only (two events; [0] and [1] read -1). Each event on
+ * the stream costs the run time. */
 int bsg_engine_profile(bsg_engine* eng, int enable);
 int bsg_engine_stage_ms(const bsg_engine* eng, float out[3]);
 /* Diagnostics of the last run: [0] jobs on the wave-per-chunk path, [1] its block threshold,
