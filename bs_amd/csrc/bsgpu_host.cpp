@@ -2,8 +2,9 @@
 // declared in include/bsgpu.h.
 //
 // A run = one launch sequence over a batch of stream segments (bsgpu_internal.h):
-//   memset(counters) → k_init → k_scan → prefix(strip counts) → k_compact → k_select
-//   → prefix(flags) → k_chunks → k_sha
+//   k_start (descriptors in, counters zeroed) → k_scan → k_refine → prefix(strip counts) →
+//   k_compact → k_select → prefix(flags) → k_chunks → … → k_sha (→ k_early_fix), with the early
+//   chains (k_pick → k_early) on a second stream from k_compact on
 // Everything after k_scan sizes itself from device-side counters, so a run never waits on the
 // host; bsg_engine_finish() is the only synchronisation (and the place where a too-small
 // candidate buffer is grown and the run repeated).
@@ -415,12 +416,16 @@ struct bsg_engine {
     // The pinned staging of the previous run may still be in flight: finish() synchronised.
     std::memcpy(h_streams.p, descs.data(), sizeof(StreamDesc) * ns);
     std::memcpy(h_strip0.p, s0.data(), sizeof(uint64_t) * (ns + 1));
-    HCHECK(hipMemcpyAsync(streams.p, h_streams.p, sizeof(StreamDesc) * ns, hipMemcpyHostToDevice,
-                          stream));
-    HCHECK(hipMemcpyAsync(strip0.p, h_strip0.p, sizeof(uint64_t) * (ns + 1),
-                          hipMemcpyHostToDevice, stream));
-    HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters) + sizeof(Early), stream));
-    HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * 2 * kLptBuckets, stream));
+    {  // descriptors in, counters and bucket counts zeroed, streams initialised: one dispatch
+      const auto* hs = static_cast<const StreamDesc*>(h_streams.dev());
+      const auto* h0 = static_cast<const uint64_t*>(h_strip0.dev());
+      if (!hs || !h0) return BSG_EDEVICE;
+      StartArgs st{hs, h0, streams.as<StreamDesc>(), strip0.as<uint64_t>(), ns,
+                   last_end.as<uint64_t>(), scount.as<uint64_t>(), carry.as<CarryOut>(),
+                   ctr.as<uint32_t>(), (uint32_t)((sizeof(Counters) + sizeof(Early)) / 4),
+                   buckets.as<uint32_t>(), 2 * kLptBuckets};
+      HCHECK(dbg("launch_start", stream, launch_start(st, stream)));
+    }
     Counters* dctr = ctr.as<Counters>();
     Early* dearly = reinterpret_cast<Early*>(ctr.as<uint8_t>() + sizeof(Counters));
     const bool early = early_ok() && total_len >= kEarlyMinBytes && strips;
@@ -441,10 +446,6 @@ struct bsg_engine {
                data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
                long_mode(), 4u * (uint32_t)num_cus, seq_wait_limit(), cand.as<uint64_t>(),
                early ? dearly : nullptr};
-
-    InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
-                carry.as<CarryOut>()};
-    if (ns) HCHECK(dbg("launch_init", stream, launch_init(ia, stream)));
 
     ScanArgs sa{};
     sa.data = d_data;
@@ -564,14 +565,15 @@ struct bsg_engine {
     HCHECK(h_streams.ensure(sizeof(StreamDesc) * nn));
     HCHECK(h_ctr.ensure(sizeof(Counters)));
     std::memcpy(h_streams.p, descs.data(), sizeof(StreamDesc) * ns);
-    HCHECK(hipMemcpyAsync(streams.p, h_streams.p, sizeof(StreamDesc) * ns, hipMemcpyHostToDevice,
-                          stream));
-    HCHECK(hipMemsetAsync(ctr.p, 0, sizeof(Counters), stream));
-    HCHECK(hipMemsetAsync(buckets.p, 0, sizeof(uint32_t) * 2 * kLptBuckets, stream));
+    {
+      const auto* hs = static_cast<const StreamDesc*>(h_streams.dev());
+      if (!hs) return BSG_EDEVICE;
+      StartArgs st{hs, nullptr, streams.as<StreamDesc>(), nullptr, ns, last_end.as<uint64_t>(),
+                   scount.as<uint64_t>(), carry.as<CarryOut>(), ctr.as<uint32_t>(),
+                   (uint32_t)(sizeof(Counters) / 4), buckets.as<uint32_t>(), 2 * kLptBuckets};
+      HCHECK(dbg("launch_start", stream, launch_start(st, stream)));
+    }
     Counters* dctr = ctr.as<Counters>();
-    InitArgs ia{streams.as<StreamDesc>(), ns, last_end.as<uint64_t>(), scount.as<uint64_t>(),
-                carry.as<CarryOut>()};
-    if (ns) HCHECK(dbg("launch_init", stream, launch_init(ia, stream)));
     mark(0);
     mark(1);  // no scan / selection stage
     ChunkArgs ca{nullptr, nullptr, nullptr, bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(),

@@ -775,7 +775,7 @@ __global__ __launch_bounds__(256) void k_tally(ChunkArgs a, uint32_t nstreams) {
     const uint64_t lo = first_chunk_of(a.bnd_info, M, s);
     const uint64_t hi = first_chunk_of(a.bnd_info, M, s + 1);
     a.scount[s] = hi - lo;
-    if (hi > lo) a.last_end[s] = a.bnd_end[hi - 1];  // else k_init's open_start stays
+    if (hi > lo) a.last_end[s] = a.bnd_end[hi - 1];  // else k_start's open_start stays
   }
 }
 
@@ -798,10 +798,20 @@ __global__ __launch_bounds__(256) void k_blob_jobs(ChunkArgs a, const StreamDesc
   }
 }
 
-__global__ void k_init(InitArgs a) {
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < a.nstreams;
-       s += gridDim.x * blockDim.x) {
-    a.last_end[s] = a.streams[s].open_start;
+__global__ __launch_bounds__(256) void k_start(StartArgs a) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  static_assert(sizeof(StreamDesc) % 16 == 0, "descriptors copy as 16-byte words");
+  const uint64_t n4 = (uint64_t)a.nstreams * (sizeof(StreamDesc) / 16);
+  const u32x4a* s4 = reinterpret_cast<const u32x4a*>(a.src);
+  u32x4a* d4 = reinterpret_cast<u32x4a*>(a.streams);
+  for (uint64_t i = t0; i < n4; i += stride) d4[i] = s4[i];
+  if (a.src_strip0)
+    for (uint64_t i = t0; i <= a.nstreams; i += stride) a.strip0[i] = a.src_strip0[i];
+  for (uint64_t i = t0; i < a.nzero0; i += stride) a.zero0[i] = 0u;
+  for (uint64_t i = t0; i < a.nzero1; i += stride) a.zero1[i] = 0u;
+  for (uint64_t s = t0; s < a.nstreams; s += stride) {
+    a.last_end[s] = a.src[s].open_start;
     a.scount[s] = 0;
     a.carry[s].valid = 0;
   }
@@ -2531,8 +2541,11 @@ hipError_t launch_blob_jobs(const ChunkArgs& a, const StreamDesc* streams, uint3
   return hipGetLastError();
 }
 
-hipError_t launch_init(const InitArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_init, dim3(grid_for(a.nstreams, 256, 1024)), dim3(256), 0, s, a);
+hipError_t launch_start(const StartArgs& a, hipStream_t s) {
+  const uint64_t work = std::max<uint64_t>(
+      std::max<uint64_t>((uint64_t)a.nstreams * (sizeof(StreamDesc) / 16), a.nstreams + 1ull),
+      std::max(a.nzero0, a.nzero1));
+  hipLaunchKernelGGL(k_start, dim3(grid_for(work, 256, 1024)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -59,12 +59,23 @@ struct ChunkArgs {
   const StreamDesc* streams;  // k_chunks: seg_base turns relative candidates into offsets
 };
 
-struct InitArgs {
-  const StreamDesc* streams;
+// k_start: a run's set-up in one dispatch (it was two H2D copies, two memsets and k_init): the
+// descriptors (and the streams' first strips) from kernel-visible pinned host memory into
+// device memory, the counters and the LPT bucket counts zeroed, each stream's open-chunk start
+// and carry state initialised.
+struct StartArgs {
+  const StreamDesc* src;        // the run's descriptors, pinned host memory (device address)
+  const uint64_t* src_strip0;   // nstreams + 1 first strips, pinned host memory; null: none
+  StreamDesc* streams;
+  uint64_t* strip0;
   uint32_t nstreams;
   uint64_t* last_end;
   uint64_t* scount;
   CarryOut* carry;
+  uint32_t* zero0;              // Counters (+ Early), zeroed
+  uint32_t nzero0;              // words
+  uint32_t* zero1;              // LPT bucket counts, zeroed
+  uint32_t nzero1;              // words
 };
 
 struct ShaArgs {
@@ -116,7 +127,7 @@ hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s);
 hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);
 hipError_t launch_chunks(const ChunkArgs& a, uint64_t cand_bound, uint32_t nstreams, hipStream_t s,
                          int num_cus);
-hipError_t launch_init(const InitArgs& a, hipStream_t s);
+hipError_t launch_start(const StartArgs& a, hipStream_t s);
 hipError_t launch_blob_jobs(const ChunkArgs& a, const StreamDesc* streams, uint32_t nstreams,
                             hipStream_t s, int num_cus);
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus);

@@ -13,7 +13,7 @@ def main(d, rep, tiles=4, skip=3):
                 key=lambda r: int(r["Start_Timestamp"]))
     cp = sorted(csv.DictReader(open(os.path.join(d, "run_memory_copy_trace.csv"))),
                 key=lambda r: int(r["Start_Timestamp"]))
-    inits = [r for r in ks if "k_init" in r["Kernel_Name"]]
+    inits = [r for r in ks if "k_init" in r["Kernel_Name"] or "k_start" in r["Kernel_Name"]]
     first = skip + rep * tiles
     # the rep's window: after the previous rep's last kernel, up to the next rep's first k_init
     lo = max(int(r["End_Timestamp"]) for r in ks if int(r["Start_Timestamp"]) < int(inits[first]["Start_Timestamp"])
@@ -26,7 +26,7 @@ def main(d, rep, tiles=4, skip=3):
     for r in ks:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         n = r["Kernel_Name"].replace("bsg::", "").split("(")[0].replace("void ", "")
-        if t0 <= s < hi and any(k in n for k in ("k_init", "k_scan", "k_sha", "k_copy_out")):
+        if t0 <= s < hi and any(k in n for k in ("k_init", "k_start", "k_scan", "k_sha", "k_copy_out")):
             ev.append((s, e, f"q{r['Queue_Id']} {n}"))
     for r in copies:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])

@@ -11,7 +11,7 @@ def main(d, rep=3, per=16):
                 key=lambda r: int(r["Start_Timestamp"]))
     cp = sorted(csv.DictReader(open(os.path.join(d, "run_memory_copy_trace.csv"))),
                 key=lambda r: int(r["Start_Timestamp"]))
-    inits = [r for r in ks if "k_init" in r["Kernel_Name"]]
+    inits = [r for r in ks if "k_init" in r["Kernel_Name"] or "k_start" in r["Kernel_Name"]]
     first = inits[rep * per]
     t0 = int(first["Start_Timestamp"])
     t_end = int(inits[(rep + 1) * per]["Start_Timestamp"]) if len(inits) > (rep + 1) * per else None

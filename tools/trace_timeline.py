@@ -10,7 +10,7 @@ def main(path):
     runs, cur = [], None
     for r in rows:
         name = r["Kernel_Name"].replace("bsg::", "").split("(")[0]
-        if name.startswith("k_init"):
+        if name.startswith(("k_init", "k_start")):
             cur = []
             runs.append(cur)
         if cur is not None and not name.startswith("__amd"):
