@@ -96,3 +96,6 @@ def test_debug_knobs_and_null_handles():
     assert L.bsg_set_stream_base(None, 1 << 40) == -22
     assert L.bsg_writer_set_stream_base(None, 1 << 40) == -22
     assert L.bsg_hasher_pinned_bytes(None) == 0
+    assert L.bsg_engine_profile(None, 2) == -22          # modes 0, 1, 2 on a real engine
+    st = (ctypes.c_float * 3)()
+    assert L.bsg_engine_stage_ms(None, st) == -22

@@ -98,3 +98,27 @@ def test_close_in_steps(gpu, oracle, table):
     e = gpu.StreamingSplitter()                      # an empty stream: nothing on the device
     assert all(len(x) == 0 for x in e.close_steps())
     e.free()
+
+
+def test_engine_profile_modes(gpu):
+    """bsg_engine_profile: 1 times every stage, 2 only the SHA-256 stage (the scan and selection
+    stages read -1), 0 off (stage_ms refused); other modes are refused."""
+    from bs_amd.synth import splitmix_array
+    L = gpu.lib()
+    data = splitmix_array(5, 3 << 20)
+    buf = gpu.DeviceBuffer(len(data) + 4096)
+    buf.from_host(data)
+    eng = gpu.Engine()
+    assert L.bsg_engine_profile(eng.h, 3) == -22 and L.bsg_engine_profile(eng.h, -1) == -22
+    for mode in (1, 2):
+        eng.profile(mode)
+        eng.run(buf.ptr, [0], [len(data)])
+        eng.finish()
+        ms = eng.stage_ms()
+        assert ms[2] > 0
+        assert (ms[0] > 0 and ms[1] > 0) if mode == 1 else (ms[0] == -1 and ms[1] == -1)
+    eng.profile(0)
+    st = (ctypes.c_float * 3)()
+    assert L.bsg_engine_stage_ms(eng.h, st) == -22
+    eng.close()
+    buf.free()
