@@ -370,6 +370,32 @@ def test_early_chains_params(gpu, oracle, table, bits, min_size):
     assert got[1][0] == want
 
 
+def test_early_chains_candidate_overflow(gpu, oracle, table):
+    """A 264 MiB run whose first 96 MiB are zeros: a candidate at every position there, far past
+    the candidate estimate, so the first run overflows (its early chains stand down) and
+    bsg_engine_finish re-runs at the exact size with the early chains on; records equal the
+    oracle's."""
+    from bs_amd.synth import splitmix_array
+    n = 264 << 20
+    host = splitmix_array(0xE0F0, n)
+    host[: 96 << 20] = 0
+    buf = gpu.DeviceBuffer(n + 4096)
+    buf.from_host(host)
+    with gpu.debug_knob(gpu.KNOB_EARLY, 1):
+        eng = gpu.Engine()
+        eng.run(buf.ptr, [0], [n])
+        eng.finish()
+        got = eng.chunks()
+        tl = eng.diag().get("timeline_us", {})
+        eng.close()
+    buf.free()
+    want = oracle.split(table, host)
+    assert len(got) == len(want)
+    for f in ("offset", "len", "level", "ref"):
+        assert (got[f] == want[f]).all(), f
+    assert tl.get("long_start", 0) < 0, tl  # the re-run's longest chunk ran early
+
+
 def test_early_chains_concurrent_engines(gpu, oracle, table):
     """Three engines on three host threads, each running a >= 256 MiB batch with early chains at
     the same time (six HIP streams over the process's hardware queues, cross-stream waits in
