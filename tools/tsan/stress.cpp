@@ -10,7 +10,8 @@
 //   - store/mem: aliased Puts of shared pieces, Seal, Delete, Get and ListRefs at once;
 //   - split::Reader (no verify) over a hand-built tree, 8 Readers with random seeks;
 //   - bsg::parallel_for (the process-wide copy pool) from 8 callers at once.
-// Mode "gpu" (on the MI355X box) adds 8 split::Writers into one MemStore and one FileStore, raw
+// Mode "gpu" (on the MI355X box) adds three engines with early chains on three threads, and
+// 8 split::Writers into one MemStore and one FileStore, raw
 // bsg_open contexts and verifying Readers, all at once (the pooled contexts and hashers).
 // Exit status 0 = every check passed; TSan reports go to stderr (halt_on_error=1 makes a race
 // fail the run).
@@ -383,6 +384,47 @@ static void gpu_writers(const std::string& root) {
   }
 }
 
+// Three engines on three threads, each a 272 MiB device-resident run twice, so the early chains
+// (a second stream, cross-stream events) run beside each other; every run's records must equal
+// the same engine's run with the early chains off.
+static void gpu_engines() {
+  const uint64_t n = 272ull << 20;
+  std::vector<std::thread> th;
+  for (int t = 0; t < 3; ++t)
+    th.emplace_back([t, n] {
+      int rc = 0;
+      bsg_engine* e = bsg_engine_create(0, nullptr, &rc);
+      CHECK(e != nullptr);
+      if (!e) return;
+      uint8_t* d = static_cast<uint8_t*>(bsg_device_malloc(0, n + BSG_READ_SLACK));
+      CHECK(d != nullptr);
+      if (!d) {
+        bsg_engine_destroy(e);
+        return;
+      }
+      CHECK(bsg_fill_splitmix(0, d, n, 0x7A5 + t, bsg_engine_stream(e)) == BSG_OK);
+      const uint64_t off = 0, len = n;
+      bsg_params p = bsg_params_default();
+      std::vector<bsg_chunk> first;
+      for (int rep = 0; rep < 3; ++rep) {
+        CHECK(bsg_engine_run(e, d, &off, &len, 1, &p) == BSG_OK);
+        uint64_t m = 0;
+        CHECK(bsg_engine_finish(e, &m) == BSG_OK);
+        std::vector<bsg_chunk> out(m);
+        CHECK(bsg_engine_copy_chunks(e, out.data(), m) == BSG_OK);
+        if (rep == 0) {
+          first = out;
+        } else {
+          CHECK(out.size() == first.size() &&
+                std::memcmp(out.data(), first.data(), out.size() * sizeof(bsg_chunk)) == 0);
+        }
+      }
+      bsg_device_free(0, d);
+      bsg_engine_destroy(e);
+    });
+  for (auto& x : th) x.join();
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "cpu";
   char tmpl[] = "/tmp/bsg_tsan_XXXXXX";
@@ -402,6 +444,8 @@ int main(int argc, char** argv) {
   if (mode == "gpu" || mode == "all") {
     gpu_writers(root);
     std::fprintf(stderr, "gpu_writers done\n");
+    gpu_engines();
+    std::fprintf(stderr, "gpu_engines done\n");
   }
   std::string rm = "rm -rf " + root;
   (void)std::system(rm.c_str());
