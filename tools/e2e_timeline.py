@@ -21,7 +21,7 @@ def main(d, rep=3, per=16):
         if s < t0 - 50_000_000 or (t_end and s > t_end):
             continue
         name = r["Kernel_Name"].replace("bsg::", "").split("(")[0].replace("void ", "")
-        if name in ("k_init", "k_scan", "k_sha") or name.startswith("__amd"):
+        if name in ("k_init", "k_start", "k_scan", "k_sha") or name.startswith("__amd"):
             ev.append((s, e, f"q{r['Queue_Id']} {name}"))
     for r in cp:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
