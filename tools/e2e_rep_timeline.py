@@ -1,7 +1,7 @@
 """Per-rep timeline of tools/e2e_trace_run.py under rocprofv3 --kernel-trace --memory-copy-trace
-(tools/gpu_e2e_trace.sh): k_start (k_init before round 4) / k_scan / k_sha / k_copy_out per queue and every H2D copy,
-relative to the rep's first H2D. Reps are told apart by their k_start count (TILES per rep, after
-SKIP k_start (k_init before round 4)s of bsg_init's warm-up runs).
+(tools/gpu_e2e_trace.sh): k_start (k_init before round 4) / k_scan / k_sha / k_copy_out per queue
+and every H2D copy, relative to the rep's first H2D. Reps are told apart by their k_start count
+(TILES per rep, after SKIP k_starts of bsg_init's warm-up runs).
   python tools/e2e_rep_timeline.py gpurun_out/e2e_trace REP [TILES=4] [SKIP=3]"""
 import csv
 import os
