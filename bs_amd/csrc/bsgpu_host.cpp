@@ -342,6 +342,7 @@ struct bsg_engine {
   hipEvent_t cand_ev = nullptr, pick_ev = nullptr, early_ev = nullptr;
   bool early_open = false;  // chains launched whose end the engine stream does not wait for yet
   static constexpr uint64_t kEarlyMinBytes = 256ull << 20;  // smaller runs: not worth a stream
+  uint64_t early_min = kEarlyMinBytes;  // bsg_init's warm-up run lowers it to load the kernels
   bool early_ok() const {
     return !snapshot && !hash_mode && knob(BSG_KNOB_EARLY) != 0;
   }
@@ -428,7 +429,7 @@ struct bsg_engine {
     }
     Counters* dctr = ctr.as<Counters>();
     Early* dearly = reinterpret_cast<Early*>(ctr.as<uint8_t>() + sizeof(Counters));
-    const bool early = early_ok() && total_len >= kEarlyMinBytes && strips;
+    const bool early = early_ok() && total_len >= early_min && strips;
     if (early) {
       if (!estream) HCHECK(stream_acquire(dev, &estream));
       // device-side dependencies only: no system-scope release (an L2 write-back) at record
@@ -1461,6 +1462,7 @@ int bsg_init(int device) {
   const uint64_t off = 0, len = kWarm;
   uint64_t n = 0;
   if (!buf) rc = BSG_ENOMEM;
+  eng->early_min = 0;  // the early-chain kernels too (they pick nothing in 64 KiB)
   if (rc == BSG_OK) rc = bsg_fill_splitmix(device, buf, kWarm, 1, eng->stream);
   if (rc == BSG_OK) rc = bsg_engine_run(eng, buf, &off, &len, 1, nullptr);
   if (rc == BSG_OK) rc = bsg_engine_finish(eng, &n);
