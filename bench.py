@@ -139,7 +139,7 @@ def cpu_threads() -> int:
     return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
 
 
-def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str):
+def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str, base=None):
     """The C oracle ("port" of the reference's per-stream Splitter + sha256: literal per-byte
     buzhash32 loop, SHA-256 with the x86 SHA extensions when the host has them, as Go's amd64
     crypto/sha256 does) over a bounded sample of the same bytes on this host. One stream per
@@ -164,9 +164,12 @@ def cpu_baseline(host_streams: list, bits: int, min_size: int, sample: str):
         nch = len(ch)
     else:
         threads = min(cpu_threads(), len(host_streams))
-        base = np.concatenate(host_streams)
         lens = [len(a) for a in host_streams]
-        off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        if base is None:
+            base = np.concatenate(host_streams)
+            off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        else:  # the streams are views of `base`
+            off = np.array([a.ctypes.data - base.ctypes.data for a in host_streams], np.uint64)
         t0 = time.perf_counter()
         ch, _ = O.split_streams(table, base, off, lens, bits=bits, min_size=min_size,
                                 threads=threads)
@@ -285,6 +288,8 @@ def pmc_traffic(kernel: str, workload: str):
     import glob
     names = KERNEL_NAMES.get(kernel, ())
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        if path.endswith("_valu_pmc.json"):  # SQ counter summaries (work_roofline), no bytes
+            continue
         try:
             with open(path) as f:
                 doc = json.load(f)
@@ -293,7 +298,7 @@ def pmc_traffic(kernel: str, workload: str):
         if not same_workload(doc.get("workload") or "", workload):
             continue
         ks = [doc.get("kernels", {}).get(n) for n in names]
-        ks = [k for k in ks if k]
+        ks = [k for k in ks if k and "hbm_bytes_per_launch" in k]
         if ks:
             return int(sum(k["hbm_bytes_per_launch"] for k in ks)), os.path.relpath(path, ROOT)
     return None, None
@@ -374,8 +379,10 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
         got = dev_ch[: len(ref)] if ns == 1 else dev_ch[: int(dev_counts[0])]
         gen_ok = bool(len(got) == len(ref) and (got["ref"] == ref["ref"]).all()
                       and (got["offset"] == ref["offset"]).all())
-    # the CPU baseline's sample: the same device bytes, copied back after timing
-    host_streams, sample, full_prefix = [], "", True
+    # the CPU baseline's sample: the same device bytes, copied back after timing. A batch is
+    # copied back whole: the baseline is timed on its first streams, the parity check below
+    # covers every stream of it.
+    host_streams, sample, full_prefix, host_all = [], "", True, None
     if rank == 0 and world == 1 and cpu_sample > 0:
         want = cpu_sample << 20
         if ns == 1:
@@ -384,7 +391,8 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
             sample = f"first {len(host_streams[0]) >> 20} MiB of stream 0"
         else:
             k = min(ns, max(4 * cpu_threads(), -(-want // nbytes)))
-            host_streams = [buf.to_host(offs[i], nbytes) for i in range(k)]
+            host_all = buf.to_host(0, offs[-1] + nbytes)
+            host_streams = [host_all[offs[i]:offs[i] + nbytes] for i in range(k)]
             sample = f"streams 0..{k - 1} of {ns} ({k} x {nbytes >> 20} MiB)"
     check_streams = []
     if world > 1 and ns == 1:  # N>1: every rank checks its own stream (no CPU baseline there)
@@ -392,10 +400,22 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
     # the engine and its input are done with: free them before the next leg
     eng.close()
     buf.free()
-    cpu, ref_ch = cpu_baseline(host_streams, bits, min_size, sample)
+    cpu, ref_ch = cpu_baseline(host_streams, bits, min_size, sample,
+                               base=host_all[:offs[len(host_streams) - 1] + nbytes]
+                               if host_all is not None else None)
     del host_streams
     ok, checked = None, ""
-    if ref_ch is not None:
+    if host_all is not None:  # every stream of the batch against the oracle, 16 threads
+        from oracle import oracle as O  # checker only, after timing
+        t0 = time.perf_counter()
+        ref_all, _ = O.split_streams(O.buzhash32_table(1), host_all, offs, lens, bits=bits,
+                                     min_size=min_size, threads=cpu_threads())
+        ok = records_match(dev_ch, dev_counts, ref_all, ns, True)
+        checked = (f"streams 0..{ns - 1} of {ns} ({ns} x {nbytes >> 20} MiB), "
+                   f"{len(ref_all)} records, oracle {time.perf_counter() - t0:.1f}s")
+        del ref_all
+        host_all = None
+    elif ref_ch is not None:
         ok = records_match(dev_ch, dev_counts, ref_ch, ns, full_prefix)
         checked = sample
     elif check_streams:
@@ -434,7 +454,50 @@ def records_match(dev, dev_counts, ref, ns: int, full: bool) -> bool:
     return all(bool((d[f] == r[f]).all()) for f in ("offset", "len", "level", "stream", "ref"))
 
 
-def roofline(workload: str, per_launch_bytes: int, stage_avg: list) -> dict:
+def pmc_valu(workload: str):
+    """Per-launch SQ counters of the SHA-256 stage's kernels from the newest committed VALU PMC
+    summary for this workload (profiles/rNN*_valu_pmc.json, tools/valu_pmc.py)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_valu_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if same_workload(doc.get("workload") or "", workload):
+            return doc.get("kernels", {}), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def work_roofline(workload: str, sha_ms: float, diag: dict) -> dict | None:
+    """The SHA-256 stage's second bound: its VALU work. achieved = the
+    VALU wave-instructions one run of the stage issues (SQ_INSTS_VALU of k_sha<false>, k_sha<true>
+    and k_early, from the committed PMC summary) / the stage's event-timed duration; peak = the
+    chip's VALU issue rate, 256 CUs x 4 SIMDs x clock / 2 cycles per wave64 instruction
+    (MI355X_MICROARCH.md: SIMD-32, a wave64 VALU op over 2 cycles) at the per-lane jobs' measured
+    clock; beside it the rate this kernel's 3-input integer ops were measured to reach on one
+    SIMD whatever the occupancy (4 cycles per wave instruction)."""
+    ks, src = pmc_valu(workload)
+    if not ks or sha_ms <= 0:
+        return None
+    names = ("void bsg::k_sha<false>(bsg::ShaArgs)", "void bsg::k_sha<true>(bsg::ShaArgs)",
+             "bsg::k_early(bsg::ShaArgs, unsigned int)")
+    insts = sum(float(ks[n]["SQ_INSTS_VALU"]) for n in names if n in ks)
+    if insts <= 0:
+        return None
+    clk = float((diag.get("lane") or {}).get("clock_ghz") or 2.4)
+    rate = insts / (sha_ms * 1e-3)
+    peak = 256 * 4 * clk * 1e9 / 2
+    peak4 = 256 * 4 * clk * 1e9 / 4
+    return {"bound": "VALU issue (per-lane SHA-256 work)", "kernel": "k_sha + k_early",
+            "valu_wave_insts_per_run": insts, "achieved": round(rate / 1e12, 4),
+            "peak": round(peak / 1e12, 4), "unit": "T wave-instructions/s",
+            "frac": round(rate / peak, 4), "clock_ghz": clk,
+            "peak_3input_measured": round(peak4 / 1e12, 4),
+            "frac_of_3input_measured": round(rate / peak4, 4), "src": src}
+
+
+def roofline(workload: str, per_launch_bytes: int, stage_avg: list, bound: str = "hbm") -> dict:
     """The dominant kernel's algorithmic bytes per launch / its event-timed duration, against
     the 8 TB/s HBM peak; k_scan beside it. traffic = HBM bytes per launch from the newest
     committed PMC summary of the same workload (profiles/rNN*_pmc.json)."""
@@ -446,7 +509,7 @@ def roofline(workload: str, per_launch_bytes: int, stage_avg: list) -> dict:
     # the SHA-256 stage runs from k_sha's launch to the end of k_early_fix, which waits for the
     # early chains (k_early, second stream, started during selection)
     kernel = "k_sha (+ the early chains' tail)" if STAGES[dom] == "k_sha" else STAGES[dom]
-    return {"bound": "hbm", "kernel": kernel,
+    return {"bound": bound, "roof": "hbm", "kernel": kernel,
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_unit": "bytes/launch", "traffic_src": traffic_src,
@@ -487,7 +550,9 @@ def main():
               "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, leg2["stage_avg"])},
               "stage_ms_src": STAGE_SRC,
               "chunks_per_step": leg2["chunks"],
-              "roofline": roofline(CONFIGS2, ns2 * n2, leg2["stage_avg"]),
+              "roofline": roofline(CONFIGS2, ns2 * n2, leg2["stage_avg"],
+                                   "serial SHA-256 chain + per-lane VALU work (HBM frac reported)"),
+              "work_roofline": work_roofline(CONFIGS2, leg2["stage_avg"][2], leg2["diag"]),
               "cpu_baseline": leg2["cpu"], "sha_path": leg2["diag"],
               "chain_roofline": chain_roofline(leg2["diag"])}
     e2e = end_to_end(args.e2e_mib, args.bits, args.min_size, local) \
@@ -517,7 +582,8 @@ def main():
                        "stream_bytes": nbytes, "streams_per_gpu": ns,
                        "split_bits": args.bits, "min_size": args.min_size, "fanout": 8,
                        "parallelism": "independent streams, one set per GPU, no collectives"},
-            "roofline": roofline(workload, ns * nbytes, stage_avg),
+            "roofline": roofline(workload, ns * nbytes, stage_avg,
+                                 "serial SHA-256 chain (HBM frac reported)"),
             "cpu_baseline": leg["cpu"],
             "end_to_end": e2e,
             "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, stage_avg)},

@@ -347,16 +347,25 @@ struct bsg_engine {
     return !snapshot && !hash_mode && knob(BSG_KNOB_EARLY) != 0;
   }
 
-  void mark(int i) {  // profile 1: every stage boundary; 2: the SHA-256 stage's two only
-    if (profile && ev[i] && (profile == 1 || i >= 2)) (void)hipEventRecord(ev[i], stream);
+  // Round 5: a lightly loaded run (at most kLightBytes, where the longest chunk's chain is the
+  // step: configs[1], [3], [4]) keeps its early chains on the engine stream right after k_pick
+  // and moves selection and k_sha to the second stream, so the chain pays no cross-stream wait
+  // (≈ 10-14 us between k_compact and k_pick, profiles/r04_run_timelines_early.txt) and no
+  // dispatch gap; selection, which has slack there, pays it instead. A loaded run (configs[2],
+  // where the hash work ends with the chain) keeps selection on the engine stream.
+  static constexpr uint64_t kLightBytes = 4ull << 30;
+
+  // profile 1: every stage boundary; 2: the SHA-256 stage's two only (on the stream it runs on)
+  void mark(int i, hipStream_t on = nullptr) {
+    if (profile && ev[i] && (profile == 1 || i >= 2)) (void)hipEventRecord(ev[i], on ? on : stream);
   }
 
   int setdev() { return herr(hipSetDevice(dev)); }
 
   int enqueue() {
     const uint32_t ns = nstreams;
-    if (early_open) {  // a failed run left early chains its engine stream never waited for
-      HCHECK(hipEventSynchronize(early_ev));
+    if (early_open) {  // a failed run left second-stream work its engine stream never waited for
+      HCHECK(hipStreamSynchronize(estream));
       early_open = false;
     }
     // strips
@@ -387,7 +396,11 @@ struct bsg_engine {
     HCHECK(streams.ensure(sizeof(StreamDesc) * (ns ? ns : 1)));
     HCHECK(strip0.ensure(sizeof(uint64_t) * (ns + 1)));
     HCHECK(counts.ensure(sizeof(uint32_t) * (strips ? strips : 1)));
-    HCHECK(refine.ensure(sizeof(uint64_t) * (strips ? strips : 1)));
+    // the refine lists (one per k_scan workgroup, scan_list_cap entries each), then their
+    // lengths (u32 per list)
+    const uint32_t lists = strips ? scan_lists(strips, num_cus) : 0;
+    const uint64_t list_cap = scan_list_cap(strips, lists);
+    HCHECK(refine.ensure(sizeof(uint64_t) * (lists * list_cap + 1) + sizeof(uint32_t) * (lists + 1)));
     HCHECK(slots.ensure(sizeof(uint32_t) * kSlotCap * (strips ? strips : 1)));
     HCHECK(strip_off.ensure(sizeof(uint64_t) * (strips ? strips : 1)));
     HCHECK(partials_a.ensure(sizeof(uint64_t) * prefix_partials_needed(strips)));
@@ -424,7 +437,9 @@ struct bsg_engine {
       StartArgs st{hs, h0, streams.as<StreamDesc>(), strip0.as<uint64_t>(), ns,
                    last_end.as<uint64_t>(), scount.as<uint64_t>(), carry.as<CarryOut>(),
                    ctr.as<uint32_t>(), (uint32_t)((sizeof(Counters) + sizeof(Early)) / 4),
-                   buckets.as<uint32_t>(), 2 * kLptBuckets};
+                   buckets.as<uint32_t>(), 2 * kLptBuckets,
+                   partials_a.as<uint32_t>(), (uint32_t)(2 * prefix_partials_needed(strips)),
+                   partials_b.as<uint32_t>(), (uint32_t)(2 * prefix_partials_needed(cand_cap))};
       HCHECK(dbg("launch_start", stream, launch_start(st, stream)));
     }
     Counters* dctr = ctr.as<Counters>();
@@ -463,6 +478,14 @@ struct bsg_engine {
     sa.cand = cand.as<uint64_t>();
     sa.cand_cap = cand_cap;
     sa.ctr = dctr;
+    sa.lists = lists;
+    sa.list_cap = list_cap;
+    sa.list_cnt = reinterpret_cast<uint32_t*>(refine.as<uint64_t>() + lists * list_cap + 1);
+    sa.dbg = nullptr;
+#ifdef BSG_SCAN_DIAG  // experiment builds: k_scan's phase stamps into the Regions debug words
+    sa.dbg = reinterpret_cast<uint64_t*>(regions.as<uint8_t>() + offsetof(Regions, wdbg));
+    HCHECK(hipMemsetAsync(sa.dbg, 0, sizeof(Regions::wdbg), stream));
+#endif
     mark(0);
     if (strips) HCHECK(dbg("launch_scan", stream, launch_scan(sa, stream, num_cus)));
     if (strips) HCHECK(dbg("launch_refine", stream, launch_refine(sa, stream, num_cus)));
@@ -478,10 +501,24 @@ struct bsg_engine {
     pa.overflow = &dctr->overflow;
     pa.cap = cand_cap;
     pa.skip_if = nullptr;
+    pa.error = &dctr->error;
     HCHECK(dbg("launch_prefix", stream, launch_prefix(pa, stream)));
 
     if (strips) HCHECK(dbg("launch_compact", stream, launch_compact(sa, stream, num_cus)));
-    if (early) {  // the sorted candidates are final: pick and start two chains beside selection
+    // (exits at once unless a strip had more candidates than slots; k_pick needs them all)
+    if (strips) HCHECK(dbg("launch_rescan", stream, launch_rescan(sa, stream, num_cus)));
+    const bool light = early && total_len <= kLightBytes;
+    hipStream_t sel_stream = stream;  // where selection and k_sha run
+    if (early && light) {  // chains on the engine stream, selection beside them
+      HCHECK(dbg("launch_pick", stream,
+                 launch_pick(cand.as<uint64_t>(), cand_cap, dctr, p.min_size, dearly, stream,
+                             num_cus)));
+      HCHECK(hipEventRecord(pick_ev, stream));
+      HCHECK(dbg("launch_early", stream, launch_early(sh, p.split_bits, stream)));
+      HCHECK(hipStreamWaitEvent(estream, pick_ev, 0));
+      sel_stream = estream;
+      early_open = true;  // until the engine stream waits for the selection stream's end
+    } else if (early) {  // the sorted candidates are final: pick and start two chains beside selection
       HCHECK(hipEventRecord(cand_ev, stream));
       HCHECK(hipStreamWaitEvent(estream, cand_ev, 0));
       HCHECK(dbg("launch_pick", estream,
@@ -493,7 +530,7 @@ struct bsg_engine {
       early_open = true;
     }
     SelArgs sel{cand.as<uint64_t>(), streams.as<StreamDesc>(), flags.as<uint32_t>(), p, dctr};
-    HCHECK(dbg("launch_select", stream, launch_select(sel, cand_cap, stream, num_cus)));
+    HCHECK(dbg("launch_select", sel_stream, launch_select(sel, cand_cap, sel_stream, num_cus)));
 
     PrefixArgs pf{};
     pf.in = flags.as<uint32_t>();
@@ -505,12 +542,13 @@ struct bsg_engine {
     pf.overflow = nullptr;
     pf.cap = 0;
     pf.skip_if = &dctr->overflow;
-    HCHECK(dbg("launch_prefix", stream, launch_prefix(pf, stream)));
+    pf.error = &dctr->error;
+    HCHECK(dbg("launch_prefix", sel_stream, launch_prefix(pf, sel_stream)));
 
     ChunkArgs ca{cand.as<uint64_t>(), flags.as<uint32_t>(), fidx.as<uint64_t>(),
                  bnd_end.as<uint64_t>(), bnd_info.as<uint64_t>(), scount.as<uint64_t>(),
                  last_end.as<uint64_t>(), chunk_cap, p, dctr, streams.as<StreamDesc>()};
-    HCHECK(dbg("launch_chunks", stream, launch_chunks(ca, cand_cap, ns, stream, num_cus)));
+    HCHECK(dbg("launch_chunks", sel_stream, launch_chunks(ca, cand_cap, ns, sel_stream, num_cus)));
     if (snapshot) {  // by kernel, not by the copy engine (see launch_copy_out)
       HCHECK(h_snap.ensure(sizeof(Counters) + 8ull * (ns ? ns : 1)));
       if (!sel_ev) HCHECK(hipEventCreateWithFlags(&sel_ev, hipEventDisableTiming));
@@ -521,11 +559,12 @@ struct bsg_engine {
       HCHECK(hipEventRecord(sel_ev, stream));
     }
 
-    if (early) HCHECK(hipStreamWaitEvent(stream, pick_ev, 0));  // k_lens reads the picks
-    HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
-    mark(2);
-    HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
-    if (early) {  // the early chains' records into place, once they are done
+    if (early && !light) HCHECK(hipStreamWaitEvent(stream, pick_ev, 0));  // k_lens reads the picks
+    HCHECK(dbg("launch_longlist", sel_stream, launch_longlist(sh, chunk_cap + ns, sel_stream, num_cus)));
+    mark(2, sel_stream);
+    HCHECK(dbg("launch_sha", sel_stream, launch_sha(sh, chunk_cap + ns, sel_stream, num_cus)));
+    if (early && light) HCHECK(hipEventRecord(early_ev, estream));  // selection + k_sha done
+    if (early) {  // the early chains' records into place, once they (and k_sha) are done
       HCHECK(hipStreamWaitEvent(stream, early_ev, 0));
       early_open = false;  // the engine stream now orders everything after the chains
       HCHECK(dbg("launch_early_fix", stream, launch_early_fix(dearly, out.as<ChunkRec>(), dctr,
@@ -571,7 +610,8 @@ struct bsg_engine {
       if (!hs) return BSG_EDEVICE;
       StartArgs st{hs, nullptr, streams.as<StreamDesc>(), nullptr, ns, last_end.as<uint64_t>(),
                    scount.as<uint64_t>(), carry.as<CarryOut>(), ctr.as<uint32_t>(),
-                   (uint32_t)(sizeof(Counters) / 4), buckets.as<uint32_t>(), 2 * kLptBuckets};
+                   (uint32_t)(sizeof(Counters) / 4), buckets.as<uint32_t>(), 2 * kLptBuckets,
+                   nullptr, 0, nullptr, 0};
       HCHECK(dbg("launch_start", stream, launch_start(st, stream)));
     }
     Counters* dctr = ctr.as<Counters>();
@@ -1388,6 +1428,7 @@ int bsg_debug_set(int k, int64_t value) {
   if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_EARLY || value < 0) return BSG_EINVAL;
   if (k == BSG_KNOB_LONG_MODE && value > 2) return BSG_EINVAL;
   if (k == BSG_KNOB_EARLY && value > 1) return BSG_EINVAL;
+  if (k == BSG_KNOB_SEQ_WAIT && value > (int64_t)UINT32_MAX) return BSG_EINVAL;  // a u32 poll count
   knob(k).store(value);
   return BSG_OK;
 }
@@ -1539,6 +1580,9 @@ void bsg_engine_destroy(bsg_engine* e) {
   if (!e) return;
   hipSetDevice(e->dev);
   if (e->stream) hipStreamSynchronize(e->stream);
+  // a failed run may have left early chains (k_pick / k_early on estream) that the engine
+  // stream never waited for: they read cand, ctr and the data, so they end before any release
+  if (e->estream) hipStreamSynchronize(e->estream);
   DevBuf* bufs[] = {&e->table, &e->streams, &e->strip0, &e->counts, &e->refine, &e->slots,
                     &e->strip_off, &e->partials_a, &e->partials_b, &e->cand, &e->flags,
                     &e->fidx, &e->bnd_end, &e->bnd_info, &e->scount, &e->last_end,
@@ -1555,10 +1599,7 @@ void bsg_engine_destroy(bsg_engine* e) {
   if (e->cand_ev) hipEventDestroy(e->cand_ev);
   if (e->pick_ev) hipEventDestroy(e->pick_ev);
   if (e->early_ev) hipEventDestroy(e->early_ev);
-  if (e->estream) {
-    hipStreamSynchronize(e->estream);
-    stream_release(e->dev, e->estream);
-  }
+  if (e->estream) stream_release(e->dev, e->estream);  // (synchronised above)
   if (e->stream) stream_release(e->dev, e->stream);
   delete e;
 }

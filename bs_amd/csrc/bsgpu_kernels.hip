@@ -297,20 +297,23 @@ __device__ __forceinline__ void hit_mark(uint32_t (&hits)[N], uint32_t b, bool h
 constexpr int kHitWords = (kStrip / 64 + 31) / 32;
 static_assert(kHitWords == 1, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
 
-template <bool WIDE>
+template <bool WIDE, bool PRE>
 __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
                                                      uint32_t lane4, const uint8_t* base,
                                                      uint32_t nfull, uint32_t& h,
-                                                     uint32_t (&hA)[64]) {
+                                                     uint32_t (&hA)[64], uint32_t (&w0)[16],
+                                                     uint32_t (&w1)[16]) {
   const uint32_t mask = a.p.mask;
   uint32_t hB[64];
   // Blocks are loaded in pairs, the two 64-byte halves of one 128-byte line back to back, so
   // the line is fetched once: loaded one block apart, the second half often found its line
   // evicted from L2 and fetched it again (k_scan read 1.5x its input on configs[1]).
-  uint32_t w0[16], w1[16], n0[16], n1[16];
+  uint32_t n0[16], n1[16];
   uint32_t hits[1] = {0};
-  scan_load16(base, w0);
-  scan_load16(base + 64ull * min(1u, nfull - 1), w1);  // (clamped, branch-free)
+  if (!PRE) {  // (PRE: the caller loaded blocks 0 and 1 beside the history block)
+    scan_load16(base, w0);
+    scan_load16(base + 64ull * min(1u, nfull - 1), w1);  // (clamped, branch-free)
+  }
   lookup64(tab, w0, hB, lane4);                         // hB = block 0
   uint32_t b = 0;
   for (; b + 1 < nfull; b += 2) {
@@ -395,39 +398,138 @@ __device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip,
   return j;
 }
 
+// Round 5: a strip's job from LDS alone. Each k_scan / k_refine workgroup caches, after strip0,
+// the two descriptor fields a strip needs (the segment's data offset; its length with the
+// finalize flag in bit 63), so the strip set-up runs no dependent global load: the round-4
+// StripJob read the descriptor from memory one strip ahead, but hipcc waited for that load
+// (vmcnt(0)) right where it was issued, a full HBM round trip at every strip start on every
+// wave of the CU.
+struct ScanStream {
+  uint64_t data_off;
+  uint64_t len_fin;   // len | finalize << 63
+};
+typedef const __attribute__((address_space(3))) ScanStream* lds_ssp;
+constexpr uint64_t kLenFin = 1ull << 63;
+
+#ifndef BSG_SCAN_SC
+#define BSG_SCAN_SC 1  // 0: strip jobs from the descriptors in global memory (round 4)
+#endif
+__device__ __forceinline__ lds_ssp cache_streams(uint32_t* lds_after, const ScanArgs& a) {
+  if (!BSG_SCAN_SC || a.nstreams + 1 > kStrip0Lds) return nullptr;
+  ScanStream* sc = reinterpret_cast<ScanStream*>(lds_after);
+  for (uint32_t i = threadIdx.x; i < a.nstreams; i += blockDim.x) {
+    const StreamDesc* sd = a.streams + i;
+    sc[i] = ScanStream{sd->data_off, sd->len | (sd->finalize ? kLenFin : 0ull)};
+  }
+  return (lds_ssp)(sc);
+}
+
+__device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip, lds_u64p s0,
+                                              lds_ssp sc) {
+  if (!sc) return strip_job(a, strip, s0);
+  const uint32_t s = find_stream(s0, a.nstreams, strip);
+  const uint64_t first = s0[s];
+  const uint64_t data_off = sc[s].data_off, len_fin = sc[s].len_fin;
+  const uint64_t seglen = len_fin & ~kLenFin;
+  StripJob j;
+  j.start = (strip - first) * (uint64_t)kStrip;
+  j.len = (uint32_t)min((uint64_t)kStrip, seglen - j.start);
+  j.d = a.data + data_off;
+  j.pre = j.start >= 64 ? j.d + j.start - 64 : a.streams[s].hist;  // an address, not a load
+  j.tail = (j.len & 63u) != 0 || (j.start + j.len == seglen && (len_fin & kLenFin) != 0);
+  return j;
+}
+
+// The hash at a strip's first byte minus one from the table values t[] of the 64 bytes before
+// it: h = XOR_k rotl(t[k], 63 - k). Independent rotates folded by xor3 (the running form,
+// h = rotl1(h) ^ t[k], is a 128-instruction dependent chain).
+template <int R>
+__device__ __forceinline__ uint32_t rotl_c(uint32_t x) {
+  if constexpr ((R & 31) == 0) return x;
+  else return __builtin_amdgcn_alignbit(x, x, 32 - (R & 31));
+}
+template <int K = 0>
+__device__ __forceinline__ uint32_t fold64(const uint32_t (&t)[64]) {
+  if constexpr (K == 64) {
+    return 0u;
+  } else {
+    return xor3(rotl_c<63 - K>(t[K]), rotl_c<62 - K>(t[K + 1]), fold64<K + 2>(t));
+  }
+}
+
 // Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
 // hit bit per block whose pre-filter fires. Writes counts[strip] = 0 and returns whether
 // k_refine has exact work for the strip (hit blocks, the segment's < 64-byte tail, or the
 // final chunk's flush), with the hit mask in *hits_out.
+#ifndef BSG_SCAN_LOAD3
+#define BSG_SCAN_LOAD3 0  // 1: the strip's first line loaded with its history block (experiment)
+#endif
+#ifndef BSG_SCAN_WARM
+#define BSG_SCAN_WARM 0  // 1: the history's lookups all issued, then folded by fold64 (round 5
+#endif                   // experiment); 0: the running form h = rotl1(h) ^ t
 template <bool WIDE>
 __device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                                           uint64_t strip, const StripJob& j, uint32_t* hits_out) {
+                                           uint64_t strip, const StripJob& j, uint32_t* hits_out,
+                                           uint64_t* t_warm) {
   uint32_t w[16];
   load16(j.pre, w);
+  const uint32_t nfull = j.len >> 6;
+  uint32_t w0[16], w1[16];
+#if BSG_SCAN_LOAD3
+  // the strip's first line in flight with its history block: one HBM round trip per strip start
+  // instead of two (a strip under 64 bytes reads within BSG_READ_SLACK)
+  scan_load16(j.d + j.start, w0);
+  scan_load16(j.d + j.start + 64ull * min(1u, nfull - 1), w1);
+  __builtin_amdgcn_sched_barrier(0);
+#endif
   uint32_t hist[64];
   uint32_t h = 0;
+#if BSG_SCAN_WARM
+#pragma unroll
+  for (int k = 0; k < 64; ++k) hist[k] = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
+  h = fold64(hist);
+#else
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
     uint32_t t = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
     h = rotl1(h) ^ t;
     hist[k] = t;
   }
-  const uint32_t nfull = j.len >> 6;
+#endif
+#ifdef BSG_SCAN_DIAG
+  *t_warm = __builtin_amdgcn_s_memtime();
+#else
+  (void)t_warm;
+#endif
   uint32_t hits = 0;
-  if (nfull) hits = scan_full_blocks<WIDE>(a, tab, lane4, j.d + j.start, nfull, h, hist);
+  if (nfull)
+    hits = scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0>(a, tab, lane4, j.d + j.start, nfull, h,
+                                                       hist, w0, w1);
   a.counts[strip] = 0u;
   *hits_out = hits;
   return hits || j.tail;
 }
 
-// Appends the flagged strips of a wave to the refine list, one atomic per wave: entry =
-// strip << 32 | hit mask.
+#ifndef BSG_SCAN_WGLIST
+#define BSG_SCAN_WGLIST 1  // refine list per k_scan workgroup, appended through an LDS counter
+#endif                     // (0: one global list, appended by a returning global atomic per wave)
+
+// Appends the flagged strips of a wave to the refine list: entry = strip << 32 | hit mask.
+// BSG_SCAN_WGLIST: to the workgroup's own list (refine + blockIdx.x * list_cap), whose count is
+// an LDS word: a returning LDS atomic instead of a returning global one, whose vmcnt(0) wait
+// also drained the next strip's prefetched lines. The workgroup stores its count at exit.
 __device__ __forceinline__ void refine_append(const ScanArgs& a, bool flag, uint64_t strip,
-                                              uint32_t hits) {
+                                              uint32_t hits, uint32_t* lds_cnt) {
   const uint64_t m = __ballot(flag);
   if (!m) return;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+#if BSG_SCAN_WGLIST
+  uint32_t b = 0;
+  if (lane == leader) b = atomicAdd(lds_cnt, (uint32_t)__builtin_popcountll(m));
+  const uint64_t base = (uint64_t)blockIdx.x * a.list_cap + (uint32_t)__shfl((int)b, (int)leader);
+#else
+  (void)lds_cnt;
   uint32_t base_lo = 0, base_hi = 0;
   if (lane == leader) {
     const uint64_t b = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->nrefine),
@@ -437,11 +539,40 @@ __device__ __forceinline__ void refine_append(const ScanArgs& a, bool flag, uint
   }
   const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)base_hi, (int)leader) << 32) |
                         (uint32_t)__shfl((int)base_lo, (int)leader);
+#endif
   if (flag) {
     const uint64_t below = m & ((1ull << lane) - 1ull);
     a.refine[base + (uint64_t)__builtin_popcountll(below)] = (strip << 32) | hits;
   }
 }
+
+// Calls f(entry) for this thread's share of the refine list(s). BSG_SCAN_WGLIST: workgroup g
+// of the consumer (k_refine, k_compact, k_rescan; their grids are ScanArgs::lists) walks k_scan
+// workgroup g's list, whose length is about the same for every list; else the grid strides
+// over the one global list.
+template <class F>
+__device__ __forceinline__ void for_refine(const ScanArgs& a, uint32_t threads, F f) {
+#if BSG_SCAN_WGLIST
+  for (uint32_t g = blockIdx.x; g < a.lists; g += gridDim.x) {
+    const uint64_t n = a.list_cnt[g];
+    const uint64_t* list = a.refine + (uint64_t)g * a.list_cap;
+    for (uint64_t i = threadIdx.x; i < n; i += threads) f(list[i]);
+  }
+#else
+  const uint64_t n = a.ctr->nrefine;
+  for (uint64_t i = (uint64_t)blockIdx.x * threads + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * threads)
+    f(a.refine[i]);
+#endif
+}
+
+// Per-wave s_memtime stamps of k_scan's phases (BSG_SCAN_DIAG experiment builds only): summed
+// over all waves into ScanArgs::dbg (tools/scan_stamps.py).
+#ifdef BSG_SCAN_DIAG
+#define SCAN_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define SCAN_STAMP(v)
+#endif
 
 // Exact candidates of one strip flagged by the fast pass, in position order: its hit blocks,
 // then the segment's tail (< 64 bytes), then Splitter.Close()'s flush of the final chunk (a
@@ -478,32 +609,88 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
   return c.count;
 }
 
+// k_scan's dynamic LDS: the table (at address 0), strip0, the stream cache, the list count.
+constexpr uint32_t kScanLdsStrip0 = kTabRows * kTabRep * 4;
+constexpr uint32_t kScanLdsStreams = kScanLdsStrip0 + kStrip0Lds * 8;
+constexpr uint32_t kScanLdsCnt = kScanLdsStreams + kStrip0Lds * (uint32_t)sizeof(ScanStream);
+constexpr uint32_t kScanLds = kScanLdsCnt + 16;
+
 // WIDE (split_bits >= 16, the packed 16-bit pre-filter) and the narrow form are separate
 // kernels, so each holds one copy of the fast loop and its registers.
+//
 template <bool WIDE>
 __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
+  SCAN_STAMP(d_t0);
+#ifdef BSG_SCAN_DIAG
+  const uint64_t d_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (!table_at_lds0(tab)) {
     if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
     return;
   }
+  uint32_t* lds_cnt = tab + kScanLdsCnt / 4;
+  if (threadIdx.x == 0) *lds_cnt = 0u;
   load_table(tab, a.table);
-  const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
+  const lds_u64p s0 = cache_strip0(tab + kScanLdsStrip0 / 4, a);
+  const lds_ssp sc = cache_streams(tab + kScanLdsStreams / 4, a);
   __syncthreads();
+  SCAN_STAMP(d_t1);
+#ifdef BSG_SCAN_DIAG
+  uint64_t d_job = 0, d_warm = 0, d_main = 0, d_app = 0, d_it = 0;
+#endif
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   uint64_t g = blockIdx.x;
   StripJob job{};
-  if (g * kScanWG + threadIdx.x < a.nstrips) job = strip_job(a, g * kScanWG + threadIdx.x, s0);
+  if (g * kScanWG + threadIdx.x < a.nstrips) job = strip_job(a, g * kScanWG + threadIdx.x, s0, sc);
   for (; g * kScanWG < a.nstrips; g += gridDim.x) {
+    SCAN_STAMP(t0);
     const uint64_t strip = g * kScanWG + threadIdx.x;
     const StripJob cur = job;
     const uint64_t next = strip + (uint64_t)gridDim.x * kScanWG;
-    if (next < a.nstrips) job = strip_job(a, next, s0);  // used one iteration later
+    if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
+    SCAN_STAMP(t1);
     bool flag = false;
     uint32_t hits = 0;
-    if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, cur, &hits);
-    refine_append(a, flag, strip, hits);
+    uint64_t t2 = 0;  // (BSG_SCAN_DIAG: the end of the history's warm-up)
+    if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, cur, &hits, &t2);
+    SCAN_STAMP(t3);
+    refine_append(a, flag, strip, hits, lds_cnt);
+    SCAN_STAMP(t4);
+#ifdef BSG_SCAN_DIAG
+    d_job += t1 - t0;
+    if (!t2) t2 = t3;  // (no strip for this wave's lane 0)
+    d_warm += t2 - t1;
+    d_main += t3 - t2;
+    d_app += t4 - t3;
+    d_it += 1;
+#endif
   }
+#if BSG_SCAN_WGLIST
+  __syncthreads();
+  if (threadIdx.x == 0) a.list_cnt[blockIdx.x] = *lds_cnt;
+#endif
+#ifdef BSG_SCAN_DIAG
+  SCAN_STAMP(d_t2);
+  if (a.dbg && (threadIdx.x & 63u) == 0) {
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(a.dbg);
+    atomicAdd(d + 0, (unsigned long long)(d_t1 - d_t0));  // prologue: table, strip0, streams
+    atomicAdd(d + 1, (unsigned long long)d_job);
+    atomicAdd(d + 2, (unsigned long long)d_warm);
+    atomicAdd(d + 3, (unsigned long long)d_main);
+    atomicAdd(d + 4, (unsigned long long)d_app);
+    atomicAdd(d + 5, (unsigned long long)(d_t2 - d_t0));  // the wave's whole life
+    atomicAdd(d + 6, (unsigned long long)d_it);
+    atomicAdd(d + 7, 1ull);                                // waves
+    atomicMax(d + 8, (unsigned long long)(d_t2 - d_t0));
+    if (threadIdx.x == 0 && blockIdx.x < 2000) {  // per workgroup: its span in cycles and in
+      d[16 + 4 * blockIdx.x] = d_t0;                  // 100 MHz realtime (the clock)
+      d[17 + 4 * blockIdx.x] = d_t2;
+      d[18 + 4 * blockIdx.x] = d_r0;
+      d[19 + 4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+#endif
 }
 
 // Exact pass over the strips k_scan listed (a few percent of them on random data at the
@@ -521,15 +708,12 @@ __global__ __launch_bounds__(kScanWG, 4) void k_refine(ScanArgs a) {
   const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
-  const uint64_t nref = a.ctr->nrefine;
-  for (uint64_t i = (uint64_t)blockIdx.x * kScanWG + threadIdx.x; i < nref;
-       i += (uint64_t)gridDim.x * kScanWG) {
-    const uint64_t e = a.refine[i];
+  for_refine(a, kScanWG, [&](uint64_t e) {
     const uint64_t strip = e >> 32;
     const uint32_t n = refine_strip<false>(a, tab, lane4, strip, (uint32_t)e, 0, s0);
     a.counts[strip] = n;
     if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
-  }
+  });
 }
 
 // Slots -> the sorted candidate list, one lane per strip. No table and no re-scan registers,
@@ -541,12 +725,10 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a) {
   const lds_u64p s0 = cache_strip0(lds, a);
   __syncthreads();
   // only strips on k_scan's refine list can hold candidates (every other count is 0)
-  const uint64_t nref = a.ctr->nrefine;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nref;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t strip = a.refine[i] >> 32;
+  for_refine(a, blockDim.x, [&](uint64_t e) {
+    const uint64_t strip = e >> 32;
     const uint32_t cnt = a.counts[strip];
-    if (cnt == 0 || cnt > (uint32_t)kSlotCap) continue;
+    if (cnt == 0 || cnt > (uint32_t)kSlotCap) return;
     const uint64_t base = a.cand_off[strip];
     uint32_t st;
     uint64_t first;
@@ -563,7 +745,7 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a) {
       if (base + i < a.cand_cap)
         a.cand[base + i] = cand_pack(st, start + (v >> 8), (v & 0x80u) != 0, v & 63u);
     }
-  }
+  });
 }
 
 // Strips with more candidates than slots (k_scan counted them in ctr->rescan) are scanned
@@ -578,14 +760,11 @@ __global__ __launch_bounds__(kScanWG, 2) void k_rescan(ScanArgs a) {
   load_table(tab, a.table);
   __syncthreads();
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
-  const uint64_t nref = a.ctr->nrefine;
-  for (uint64_t i = (uint64_t)blockIdx.x * kScanWG + threadIdx.x; i < nref;
-       i += (uint64_t)gridDim.x * kScanWG) {
-    const uint64_t e = a.refine[i];
+  for_refine(a, kScanWG, [&](uint64_t e) {
     const uint64_t strip = e >> 32;
     if (a.counts[strip] > (uint32_t)kSlotCap)
       refine_strip<true>(a, tab, lane4, strip, (uint32_t)e, a.cand_off[strip], nullptr);
-  }
+  });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -677,6 +856,107 @@ __global__ __launch_bounds__(kScanT) void k_prefix_down(PrefixArgs a) {
   // Offsets are only read where the input is non-zero (k_compact / k_rescan for strips with
   // candidates, k_chunks for flagged candidates), so only those are written: on configs[2]
   // this is ~250 K of 8 M strip offsets.
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (first + i < n && v[i]) a.out[first + i] = pre;
+    pre += v[i];
+  }
+}
+
+// Single-pass exclusive prefix (round 5; decoupled look-back): one dispatch instead of
+// k_prefix_reduce -> k_prefix_top -> k_prefix_down, each of which cost a kernel boundary and a
+// pass over the input on the way to the early chains (configs[2]: 48 us for the strip counts).
+// Workgroup t takes tile t, publishes its tile's sum, and wave 0 looks back over the preceding
+// tiles 64 at a time, summing published tile sums until it meets a tile's published inclusive
+// prefix. Tiles go by blockIdx, not by a ticket counter: one counter hands out ≈ 88 tickets per
+// us (MI355X_MICROARCH.md, dequeue), 47 us for configs[2]'s 4,096 tiles, which made this kernel
+// slower than the three it replaces (profiles/r05_ab2.log). A workgroup waits only for tiles of
+// lower index, which the dispatcher has placed before it. A status word carries its value with its flag (the value in
+// the low 62 bits), so one relaxed agent-scope (sc1) store publishes it and one such load reads
+// it: no payload to fence. k_start zeroes the status words. A bounded poll flags a device error.
+constexpr uint64_t kPfxAgg = 1ull << 62, kPfxInc = 2ull << 62, kPfxVal = kPfxAgg - 1;
+constexpr uint32_t kPfxPolls = 1u << 22;
+
+__device__ __forceinline__ uint64_t pfx_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pfx_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kScanT) void k_prefix1(PrefixArgs a, uint64_t ntiles) {
+  __shared__ uint64_t wsum[kScanT / 64];
+  __shared__ uint64_t sh_excl;
+  if (a.skip_if && *a.skip_if) return;
+  const uint64_t n = scan_n(a);
+  uint64_t* status = a.partials;
+  (void)ntiles;
+  const uint64_t t = blockIdx.x;
+  const uint64_t base = t * (uint64_t)kScanTile;
+  if (base >= n && t != 0) return;  // past the data: nobody looks back at this tile
+  const uint64_t first = base + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = (first + i < n) ? a.in[first + i] : 0u;
+    sum += v[i];
+  }
+  uint64_t x = sum;  // inclusive wave scan
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o);
+    if ((threadIdx.x & 63) >= (uint32_t)o) x += y;
+  }
+  if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint64_t pre = x - sum;
+  const uint32_t w = threadIdx.x >> 6;
+  for (uint32_t k = 0; k < w; ++k) pre += wsum[k];
+  const uint64_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (w == 0) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t excl = 0;
+    if (t == 0) {
+      if (lane == 0) pfx_store(status, kPfxInc | agg);
+    } else {
+      if (lane == 0) pfx_store(status + t, kPfxAgg | agg);
+      int64_t p = (int64_t)t - 1;  // the window's newest tile
+      bool done = false;
+      uint32_t polls = 0;
+      while (!done) {
+        const int64_t q = p - (int64_t)lane;  // this lane's predecessor
+        uint64_t st = q >= 0 ? pfx_load(status + q) : kPfxInc;  // (before tile 0: nothing)
+        while (__ballot(st == 0)) {  // someone's predecessor has not published yet
+          if (++polls > kPfxPolls) {
+            if (lane == 0 && a.error) atomicOr(reinterpret_cast<unsigned long long*>(a.error), 32ull);
+            st = kPfxInc;  // give up (the run is flagged)
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          if (st == 0) st = pfx_load(status + q);
+        }
+        // the nearest predecessor with an inclusive prefix ends the look-back
+        const uint64_t inc = __ballot((st & kPfxInc) != 0);
+        const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        uint64_t part = (lane <= stop) ? (st & kPfxVal) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        excl += part;
+        done = inc != 0;
+        p -= 64;
+      }
+      if (lane == 0) pfx_store(status + t, kPfxInc | (excl + agg));
+    }
+    if (lane == 0) {
+      sh_excl = excl;
+      if (n == 0 || (base < n && n <= base + kScanTile)) {  // the last tile: the total
+        *a.total = excl + agg;
+        if (a.overflow && excl + agg > a.cap) *a.overflow = 1;
+      }
+    }
+  }
+  __syncthreads();
+  pre += sh_excl;
+  // offsets only where the input is non-zero (the only offsets ever read, as k_prefix_down)
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
     if (first + i < n && v[i]) a.out[first + i] = pre;
@@ -810,6 +1090,8 @@ __global__ __launch_bounds__(256) void k_start(StartArgs a) {
     for (uint64_t i = t0; i <= a.nstreams; i += stride) a.strip0[i] = a.src_strip0[i];
   for (uint64_t i = t0; i < a.nzero0; i += stride) a.zero0[i] = 0u;
   for (uint64_t i = t0; i < a.nzero1; i += stride) a.zero1[i] = 0u;
+  for (uint64_t i = t0; i < a.nzero2; i += stride) a.zero2[i] = 0u;
+  for (uint64_t i = t0; i < a.nzero3; i += stride) a.zero3[i] = 0u;
   for (uint64_t s = t0; s < a.nstreams; s += stride) {
     a.last_end[s] = a.src[s].open_start;
     a.scount[s] = 0;
@@ -2389,10 +2671,15 @@ __global__ __launch_bounds__(256, 1) void k_early(ShaArgs a, uint32_t split_bits
 
 // After k_sha and k_early: the early chunks' records into their places (k_lens matched them to
 // their job indices), and the longest one's timing stamps into the counters.
+// A pick that k_lens did not match was hashed by k_sha as usual, but it means the pick rule and
+// the selection disagree about a chunk: a bug, flagged as a device error (bit 16) so that no
+// test passes over it.
 __global__ void k_early_fix(Early* e, ChunkRec* out, Counters* ctr) {
   if (ctr->overflow || ctr->error) return;
   const int k = threadIdx.x;
   if (k < kEarly && e->top[k] && e->idx[k]) out[e->idx[k] - 1] = e->rec[k];
+  if (k < kEarly && e->top[k] && !e->idx[k])
+    atomicOr(reinterpret_cast<unsigned long long*>(&ctr->error), 16ull);
   if (k == 0 && e->top[0] && e->idx[0])
     for (int i = 0; i < 5; ++i) ctr->diag[i] = e->diag[i];
 }
@@ -2476,38 +2763,70 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
 #ifndef BSG_SCAN_GRID
 #define BSG_SCAN_GRID 2  // k_scan workgroups per CU in the grid (one is resident at a time)
 #endif
+uint32_t scan_lists(uint64_t nstrips, int num_cus) {
+  const uint64_t groups = (nstrips + kScanWG - 1) / kScanWG;
+  return grid_for(groups, 1, (uint32_t)BSG_SCAN_GRID * (uint32_t)num_cus);
+}
+
+uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists) {
+  const uint64_t groups = (nstrips + kScanWG - 1) / kScanWG;
+  return lists ? (groups + lists - 1) / lists * (uint64_t)kScanWG : 0;
+}
+
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
-  const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
-  const uint32_t grid = grid_for(groups, 1, (uint32_t)BSG_SCAN_GRID * (uint32_t)num_cus);
+  const uint32_t grid = scan_lists(a.nstrips, num_cus);
+  if (grid != a.lists) return hipErrorInvalidValue;  // the refine lists assume this grid
+  static_assert(kScanLds <= 160 * 1024, "k_scan LDS");
   if (a.p.split_bits >= 16)
-    hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
+    hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWG), kScanLds, s, a);
   else
-    hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
+    hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWG), kScanLds, s, a);
   return hipGetLastError();
 }
 
+// The refine-list consumers: one workgroup per list (BSG_SCAN_WGLIST), else a grid-stride walk.
+static uint32_t refine_grid(const ScanArgs& a, uint32_t per_wg, uint32_t cap) {
+#if BSG_SCAN_WGLIST
+  (void)per_wg;
+  (void)cap;
+  return a.lists;
+#else
+  return grid_for(a.nstrips, per_wg, cap);
+#endif
+}
+
 hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus) {
-  const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
-  const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
+  const uint32_t grid = refine_grid(a, (uint32_t)kScanWG, 2u * (uint32_t)num_cus);
   hipLaunchKernelGGL(k_refine, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus) {
-  const uint64_t groups = (a.nstrips + kScanWG - 1) / kScanWG;
-  const uint32_t grid = grid_for(groups, 1, 2u * (uint32_t)num_cus);
-  const uint32_t cgrid = grid_for(a.nstrips, 256, 16u * (uint32_t)num_cus);
+  const uint32_t cgrid = refine_grid(a, 256, 16u * (uint32_t)num_cus);
   hipLaunchKernelGGL(k_compact, dim3(cgrid), dim3(256), kStrip0Lds * 8, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rescan(const ScanArgs& a, hipStream_t s, int num_cus) {
+  const uint32_t grid = refine_grid(a, (uint32_t)kScanWG, 2u * (uint32_t)num_cus);
   hipLaunchKernelGGL(k_rescan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
   return hipGetLastError();
 }
 
 uint64_t prefix_partials_needed(uint64_t n_bound) {
-  return (n_bound + kScanTile - 1) / kScanTile + 1;
+  return (n_bound + kScanTile - 1) / kScanTile + 2;  // tiles (at least one), then the ticket
 }
 
+#ifndef BSG_PREFIX1
+#define BSG_PREFIX1 1  // the single-pass prefix (0: three kernels, round 4)
+#endif
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s) {
   const uint64_t nb = (a.n_bound + kScanTile - 1) / kScanTile;
+#if BSG_PREFIX1
+  // status words [0, nb) and the ticket at [nb], zeroed by k_start (prefix_partials_needed)
+  hipLaunchKernelGGL(k_prefix1, dim3((uint32_t)(nb ? nb : 1)), dim3(kScanT), 0, s, a, nb ? nb : 1);
+  return hipGetLastError();
+#endif
   if (nb == 0) {
     hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(1024), 0, s, a, (uint64_t)0);
     return hipGetLastError();
@@ -2544,7 +2863,7 @@ hipError_t launch_blob_jobs(const ChunkArgs& a, const StreamDesc* streams, uint3
 hipError_t launch_start(const StartArgs& a, hipStream_t s) {
   const uint64_t work = std::max<uint64_t>(
       std::max<uint64_t>((uint64_t)a.nstreams * (sizeof(StreamDesc) / 16), a.nstreams + 1ull),
-      std::max(a.nzero0, a.nzero1));
+      std::max(std::max(a.nzero0, a.nzero1), std::max(a.nzero2, a.nzero3)));
   hipLaunchKernelGGL(k_start, dim3(grid_for(work, 256, 1024)), dim3(256), 0, s, a);
   return hipGetLastError();
 }

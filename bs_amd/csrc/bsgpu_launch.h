@@ -16,14 +16,23 @@ struct ScanArgs {
   const uint32_t* table;    // 256 buzhash32 entries
   Params p;
   uint32_t* counts;         // [nstrips]
-  uint64_t* refine;         // [nstrips] strips k_refine must scan exactly: strip << 32 | the
-                            // fast pass's hit mask (one bit per 64-byte block); ctr->nrefine
+  uint64_t* refine;         // [lists * list_cap] strips k_refine must scan exactly: strip << 32 |
+                            // the fast pass's hit mask (one bit per 64-byte block); k_scan
+                            // workgroup g appends to refine + g * list_cap (BSG_SCAN_WGLIST)
   uint32_t* slots;          // [nstrips * kSlotCap]
   const uint64_t* cand_off; // [nstrips] exclusive candidate offsets (compact)
   uint64_t* cand;           // [cand_cap]
   uint64_t cand_cap;
   Counters* ctr;
+  uint32_t lists;           // k_scan's grid = the number of refine lists (scan_lists())
+  uint64_t list_cap;        // entries per list: the strips one k_scan workgroup scans, at most
+  uint32_t* list_cnt;       // [lists] each list's length, stored by its workgroup at exit
+  uint64_t* dbg;            // BSG_SCAN_DIAG builds: k_scan's phase stamps (else null)
 };
+// k_scan's grid for nstrips strips (its workgroups loop over 512-strip groups) and the length
+// bound of each workgroup's refine list; the host sizes ScanArgs::refine with them.
+uint32_t scan_lists(uint64_t nstrips, int num_cus);
+uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists);
 
 struct PrefixArgs {
   const uint32_t* in;
@@ -35,6 +44,7 @@ struct PrefixArgs {
   uint64_t* overflow;       // optional: set to 1 when total > cap
   uint64_t cap;
   const uint64_t* skip_if;  // optional: skip when *skip_if != 0
+  uint64_t* error;          // k_prefix1: Counters::error (|= 32: a look-back poll timed out)
 };
 
 struct SelArgs {
@@ -76,6 +86,10 @@ struct StartArgs {
   uint32_t nzero0;              // words
   uint32_t* zero1;              // LPT bucket counts, zeroed
   uint32_t nzero1;              // words
+  uint32_t* zero2;              // the two prefixes' status words (k_prefix1), zeroed
+  uint32_t nzero2;              // words
+  uint32_t* zero3;
+  uint32_t nzero3;
 };
 
 struct ShaArgs {
@@ -122,6 +136,7 @@ struct BlobShaArgs {
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus);
 hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus);
 hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus);
+hipError_t launch_rescan(const ScanArgs& a, hipStream_t s, int num_cus);
 uint64_t prefix_partials_needed(uint64_t n_bound);
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s);
 hipError_t launch_select(const SelArgs& a, uint64_t cand_bound, hipStream_t s, int num_cus);

@@ -22,19 +22,27 @@ def main():
     mv = memoryview(data)
     bsgpu.init(0)
     w = bsgpu.StreamingSplitter(tile=tile)
+    clk = time.CLOCK_BOOTTIME if os.environ.get("E2E_CLOCK", "boot") == "boot" else time.CLOCK_MONOTONIC
+    now = lambda: time.clock_gettime_ns(clk)  # noqa: E731  (the tracer's clock: host stamps line up)
     for rep in range(int(os.environ.get("E2E_REPS", "5"))):
         w.reset()
         t0 = time.perf_counter()
+        stamps = [("start", now())]
         nch = 0
         for i in range(0, n, piece):
             w.write(mv[i:i + piece])
+            stamps.append(("write", now()))
             nch += len(w.drain())
+            stamps.append(("drain", now()))
         tw = time.perf_counter() - t0
         w.close()
+        stamps.append(("close", now()))
         nch += len(w.drain())
+        stamps.append(("end", now()))
         dt = time.perf_counter() - t0
         print(json.dumps({"rep": rep, "seconds": round(dt, 4), "write_phase_s": round(tw, 4),
-                          "chunks": nch, "gib_per_s": round(n / dt / 2**30, 3)}), flush=True)
+                          "chunks": nch, "gib_per_s": round(n / dt / 2**30, 3),
+                          "host_ns": stamps}), flush=True)
     w.free()
 
 

@@ -6,4 +6,6 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 OUT=${OUT:-e2e_trace}
-timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/$OUT -o run -- python3 tools/e2e_trace_run.py > gpurun_out/$OUT.log 2>&1 || exit $?
+TRACE="--kernel-trace --memory-copy-trace"
+[ "${HIP_TRACE:-0}" = 1 ] && TRACE="$TRACE --hip-trace"
+timeout -k 10 240 rocprofv3 $TRACE --output-format csv -d gpurun_out/$OUT -o run -- python3 tools/e2e_trace_run.py > gpurun_out/$OUT.log 2>&1 || exit $?
