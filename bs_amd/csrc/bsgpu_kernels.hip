@@ -101,16 +101,17 @@ __device__ __forceinline__ uint32_t lookup(const uint32_t* tab, uint32_t w, uint
 // each uint4 store writes 4 replicas of one row. A thread issues all of its loads before its
 // stores: as a load-store loop, each of the 8 iterations waited for its global load (~8
 // dependent L2 round trips at the start of every workgroup, before any scanning).
+template <uint32_t NT = kScanWG>
 __device__ __forceinline__ void load_table(uint32_t* tab, const uint32_t* __restrict__ T) {
   constexpr uint32_t kVec = kTabRows * kTabRep / 4;
-  constexpr uint32_t kPer = kVec / kScanWG;
-  static_assert(kVec % kScanWG == 0, "table stores per thread");
+  constexpr uint32_t kPer = kVec / NT;
+  static_assert(kVec % NT == 0, "table stores per thread");
   u32x4a* t4 = reinterpret_cast<u32x4a*>(tab);
   uint32_t v[kPer];
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) v[k] = T[(threadIdx.x + k * kScanWG) >> 4];
+  for (uint32_t k = 0; k < kPer; ++k) v[k] = T[(threadIdx.x + k * NT) >> 4];
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) t4[threadIdx.x + k * kScanWG] = u32x4a{v[k], v[k], v[k], v[k]};
+  for (uint32_t k = 0; k < kPer; ++k) t4[threadIdx.x + k * NT] = u32x4a{v[k], v[k], v[k], v[k]};
 }
 
 template <class P>
@@ -342,8 +343,9 @@ __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const ui
 constexpr uint32_t kStrip0Lds = 2048;
 typedef const __attribute__((address_space(3))) uint64_t* lds_u64p;
 
-__device__ __forceinline__ lds_u64p cache_strip0(uint32_t* lds_after, const ScanArgs& a) {
-  if (a.nstreams + 1 > kStrip0Lds) return nullptr;
+__device__ __forceinline__ lds_u64p cache_strip0(uint32_t* lds_after, const ScanArgs& a,
+                                                 uint32_t cap = kStrip0Lds) {
+  if (a.nstreams + 1 > cap) return nullptr;
   uint64_t* s0 = reinterpret_cast<uint64_t*>(lds_after);
   for (uint32_t i = threadIdx.x; i <= a.nstreams; i += blockDim.x) s0[i] = a.strip0[i];
   return (lds_u64p)(s0);  // generic -> LDS address space
@@ -462,7 +464,7 @@ __device__ __forceinline__ uint32_t fold64(const uint32_t (&t)[64]) {
 // k_refine has exact work for the strip (hit blocks, the segment's < 64-byte tail, or the
 // final chunk's flush), with the hit mask in *hits_out.
 #ifndef BSG_SCAN_LOAD3
-#define BSG_SCAN_LOAD3 0  // 1: the strip's first line loaded with its history block (experiment)
+#define BSG_SCAN_LOAD3 1  // the strip's first line loaded with its history block (0: round 4)
 #endif
 #ifndef BSG_SCAN_WARM
 #define BSG_SCAN_WARM 0  // 1: the history's lookups all issued, then folded by fold64 (round 5
@@ -510,6 +512,9 @@ __device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* ta
   return hits || j.tail;
 }
 
+#ifndef BSG_SCAN_FUSE
+#define BSG_SCAN_FUSE 1  // k_scan workgroups refine their own lists (0: a k_refine dispatch)
+#endif
 #ifndef BSG_SCAN_WGLIST
 #define BSG_SCAN_WGLIST 1  // refine list per k_scan workgroup, appended through an LDS counter
 #endif                     // (0: one global list, appended by a returning global atomic per wave)
@@ -609,17 +614,30 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
   return c.count;
 }
 
-// k_scan's dynamic LDS: the table (at address 0), strip0, the stream cache, the list count.
+// k_scan's workgroup (BSG_SCAN_WGS threads, a strip each per iteration) and dynamic LDS: the
+// table (at address 0), strip0, the stream cache, the list count. A 256-thread workgroup (one
+// wave per SIMD) runs two per CU, so a CU's next workgroup starts when one ends instead of when
+// the CU's only one does (its slowest wave ends ~10 % after the average, profiles/r05_scan_stamps*);
+// two must fit the CU's 160 KiB: no stream cache, and strip0 two entries short for the count.
+#ifndef BSG_SCAN_WGS
+#define BSG_SCAN_WGS 256
+#endif
+constexpr uint32_t kScanThreads = BSG_SCAN_WGS;
+static_assert(kScanThreads == 512 || kScanThreads == 256, "k_scan workgroup size");
+constexpr bool kScanPair = kScanThreads == 256;  // two workgroups per CU
+constexpr uint32_t kScanStrip0Cap = kScanPair ? kStrip0Lds - 2 : kStrip0Lds;
 constexpr uint32_t kScanLdsStrip0 = kTabRows * kTabRep * 4;
-constexpr uint32_t kScanLdsStreams = kScanLdsStrip0 + kStrip0Lds * 8;
-constexpr uint32_t kScanLdsCnt = kScanLdsStreams + kStrip0Lds * (uint32_t)sizeof(ScanStream);
-constexpr uint32_t kScanLds = kScanLdsCnt + 16;
+constexpr uint32_t kScanLdsStreams = kScanLdsStrip0 + kScanStrip0Cap * 8;
+constexpr uint32_t kScanLdsCnt =
+    kScanLdsStreams + (kScanPair ? 0u : kStrip0Lds * (uint32_t)sizeof(ScanStream));
+constexpr uint32_t kScanLds = kScanLdsCnt + (kScanPair ? 4u : 16u);
+static_assert(!kScanPair || 2 * kScanLds <= 160 * 1024, "two k_scan workgroups per CU");
 
 // WIDE (split_bits >= 16, the packed 16-bit pre-filter) and the narrow form are separate
 // kernels, so each holds one copy of the fast loop and its registers.
 //
 template <bool WIDE>
-__global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
+__global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
   SCAN_STAMP(d_t0);
 #ifdef BSG_SCAN_DIAG
@@ -631,9 +649,9 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   }
   uint32_t* lds_cnt = tab + kScanLdsCnt / 4;
   if (threadIdx.x == 0) *lds_cnt = 0u;
-  load_table(tab, a.table);
-  const lds_u64p s0 = cache_strip0(tab + kScanLdsStrip0 / 4, a);
-  const lds_ssp sc = cache_streams(tab + kScanLdsStreams / 4, a);
+  load_table<kScanThreads>(tab, a.table);
+  const lds_u64p s0 = cache_strip0(tab + kScanLdsStrip0 / 4, a, kScanStrip0Cap);
+  const lds_ssp sc = kScanPair ? nullptr : cache_streams(tab + kScanLdsStreams / 4, a);
   __syncthreads();
   SCAN_STAMP(d_t1);
 #ifdef BSG_SCAN_DIAG
@@ -642,12 +660,13 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   uint64_t g = blockIdx.x;
   StripJob job{};
-  if (g * kScanWG + threadIdx.x < a.nstrips) job = strip_job(a, g * kScanWG + threadIdx.x, s0, sc);
-  for (; g * kScanWG < a.nstrips; g += gridDim.x) {
+  if (g * kScanThreads + threadIdx.x < a.nstrips)
+    job = strip_job(a, g * kScanThreads + threadIdx.x, s0, sc);
+  for (; g * kScanThreads < a.nstrips; g += gridDim.x) {
     SCAN_STAMP(t0);
-    const uint64_t strip = g * kScanWG + threadIdx.x;
+    const uint64_t strip = g * kScanThreads + threadIdx.x;
     const StripJob cur = job;
-    const uint64_t next = strip + (uint64_t)gridDim.x * kScanWG;
+    const uint64_t next = strip + (uint64_t)gridDim.x * kScanThreads;
     if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
     SCAN_STAMP(t1);
     bool flag = false;
@@ -668,7 +687,25 @@ __global__ __launch_bounds__(kScanWG, 2) void k_scan(ScanArgs a) {
   }
 #if BSG_SCAN_WGLIST
   __syncthreads();
-  if (threadIdx.x == 0) a.list_cnt[blockIdx.x] = *lds_cnt;
+  const uint32_t nlist = *lds_cnt;
+  if (threadIdx.x == 0) a.list_cnt[blockIdx.x] = nlist;
+#if BSG_SCAN_FUSE
+  // k_refine's exact pass over this workgroup's own list, here, with the table and strip0
+  // already in LDS: no dispatch, no table load, and a workgroup that ends early refines while
+  // the others still scan. (The list entries are this workgroup's own stores, ordered by the
+  // barrier above.)
+  {
+    const uint64_t* list = a.refine + (uint64_t)blockIdx.x * a.list_cap;
+    for (uint32_t i = threadIdx.x; i < nlist; i += kScanThreads) {
+      const uint64_t e = list[i];
+      const uint64_t strip = e >> 32;
+      const uint32_t n = refine_strip<false>(a, tab, lane4, strip, (uint32_t)e, 0, s0);
+      a.counts[strip] = n;
+      if (n > (uint32_t)kSlotCap)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
+    }
+  }
+#endif
 #endif
 #ifdef BSG_SCAN_DIAG
   SCAN_STAMP(d_t2);
@@ -2764,13 +2801,13 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
 #define BSG_SCAN_GRID 2  // k_scan workgroups per CU in the grid (one is resident at a time)
 #endif
 uint32_t scan_lists(uint64_t nstrips, int num_cus) {
-  const uint64_t groups = (nstrips + kScanWG - 1) / kScanWG;
-  return grid_for(groups, 1, (uint32_t)BSG_SCAN_GRID * (uint32_t)num_cus);
+  const uint64_t groups = (nstrips + kScanThreads - 1) / kScanThreads;
+  return grid_for(groups, 1, (uint32_t)BSG_SCAN_GRID * (kScanPair ? 2u : 1u) * (uint32_t)num_cus);
 }
 
 uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists) {
-  const uint64_t groups = (nstrips + kScanWG - 1) / kScanWG;
-  return lists ? (groups + lists - 1) / lists * (uint64_t)kScanWG : 0;
+  const uint64_t groups = (nstrips + kScanThreads - 1) / kScanThreads;
+  return lists ? (groups + lists - 1) / lists * (uint64_t)kScanThreads : 0;
 }
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
@@ -2778,9 +2815,9 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
   if (grid != a.lists) return hipErrorInvalidValue;  // the refine lists assume this grid
   static_assert(kScanLds <= 160 * 1024, "k_scan LDS");
   if (a.p.split_bits >= 16)
-    hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanWG), kScanLds, s, a);
+    hipLaunchKernelGGL(k_scan<true>, dim3(grid), dim3(kScanThreads), kScanLds, s, a);
   else
-    hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanWG), kScanLds, s, a);
+    hipLaunchKernelGGL(k_scan<false>, dim3(grid), dim3(kScanThreads), kScanLds, s, a);
   return hipGetLastError();
 }
 
@@ -2796,6 +2833,12 @@ static uint32_t refine_grid(const ScanArgs& a, uint32_t per_wg, uint32_t cap) {
 }
 
 hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus) {
+#if BSG_SCAN_FUSE && BSG_SCAN_WGLIST
+  (void)a;
+  (void)s;
+  (void)num_cus;
+  return hipSuccess;  // k_scan did it
+#endif
   const uint32_t grid = refine_grid(a, (uint32_t)kScanWG, 2u * (uint32_t)num_cus);
   hipLaunchKernelGGL(k_refine, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
   return hipGetLastError();
