@@ -10,7 +10,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libbsgpu.so")
 SOURCES = ["bsgpu_kernels.hip", "bsgpu_host.cpp", "bs_split.cpp", "bs_filestore.cpp"]
 HEADERS = ["bsgpu_internal.h", "host_pool.h", "bsgpu_launch.h", "buzhash32_table.inc", "sha256_device.h",
-           "sha256_skew_block.inc", "sha256_skew_loop.inc", "sha256_oct_loop.inc"]
+           "sha256_skew_block.inc", "sha256_skew_loop.inc", "sha256_oct_loop.inc",
+           "sha256_lane_asm.inc"]
 ARCH = os.environ.get("BSG_OFFLOAD_ARCH", "gfx950")
 
 

@@ -110,8 +110,10 @@ struct Counters {
   uint64_t tickets_grp;        //   runs on pair tickets (kPairGroup jobs, one lane pair each)
   uint64_t nrefine;            // strips k_scan listed for the exact pass (k_refine)
   uint64_t helped;             // solo tickets [0, helped) run with a helper wave (k_sha)
+  uint64_t scan_ticket;        // k_scan's strip groups handed out past the first (BSG_SCAN_DYN)
+  uint64_t pad[7];
 };
-static_assert(sizeof(Counters) == 256, "Counters layout");
+static_assert(sizeof(Counters) == 320, "Counters layout");
 
 // Per-lane job descriptor (k_lens writes one per job): per-lane mode prefetches it a few blocks
 // before its current job ends, so starting the next job costs no dependent loads.

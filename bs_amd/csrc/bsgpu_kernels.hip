@@ -622,6 +622,17 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
 #ifndef BSG_SCAN_WGS
 #define BSG_SCAN_WGS 256
 #endif
+// BSG_SCAN_DYN: the grid is what the chip holds at once (two workgroups per CU) and each
+// workgroup takes its next strip group from a ticket counter (Counters::scan_ticket) instead of
+// the fixed stride, so the workgroups of slow CUs take fewer groups and all end together. With
+// the fixed stride, 1,024 workgroups ran as two rounds of 512 and the step ended with the slowest
+// workgroup of the second round: wave life 1.61 ms on average, 2.05 at most, the kernel 3.6 ms
+// on configs[2] (profiles/r05_scan_stamps5_w256.log). A workgroup takes at most kScanDynShare
+// times its even share, which bounds its refine list.
+#ifndef BSG_SCAN_DYN
+#define BSG_SCAN_DYN 1
+#endif
+constexpr uint64_t kScanDynShare = 2;
 constexpr uint32_t kScanThreads = BSG_SCAN_WGS;
 static_assert(kScanThreads == 512 || kScanThreads == 256, "k_scan workgroup size");
 constexpr bool kScanPair = kScanThreads == 256;  // two workgroups per CU
@@ -630,7 +641,7 @@ constexpr uint32_t kScanLdsStrip0 = kTabRows * kTabRep * 4;
 constexpr uint32_t kScanLdsStreams = kScanLdsStrip0 + kScanStrip0Cap * 8;
 constexpr uint32_t kScanLdsCnt =
     kScanLdsStreams + (kScanPair ? 0u : kStrip0Lds * (uint32_t)sizeof(ScanStream));
-constexpr uint32_t kScanLds = kScanLdsCnt + (kScanPair ? 4u : 16u);
+constexpr uint32_t kScanLds = kScanLdsCnt + 16u;  // the list count, 2 ticket slots
 static_assert(!kScanPair || 2 * kScanLds <= 160 * 1024, "two k_scan workgroups per CU");
 
 // WIDE (split_bits >= 16, the packed 16-bit pre-filter) and the narrow form are separate
@@ -662,12 +673,43 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   StripJob job{};
   if (g * kScanThreads + threadIdx.x < a.nstrips)
     job = strip_job(a, g * kScanThreads + threadIdx.x, s0, sc);
+#if BSG_SCAN_DYN
+  // group tickets: the first group is blockIdx.x, later ones gridDim.x + the counter's value.
+  // Thread 0 takes the ticket after next while the current group is scanned; it reaches the
+  // others through LDS slot (iteration & 1) behind the iteration's barrier (a slot is written
+  // again two iterations later, after every thread has passed the barrier that follows its reads).
+  const uint64_t ngroups = (a.nstrips + kScanThreads - 1) / kScanThreads;
+  const uint64_t max_groups = a.list_cap / kScanThreads;  // the refine list's bound
+  uint32_t* tslot = lds_cnt + 1;
+  uint64_t taken = 1;
+  uint64_t gnext = ~0ull;
+  if (threadIdx.x == 0) {
+    const uint64_t t = taken < max_groups
+        ? gridDim.x + atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->scan_ticket), 1ull)
+        : ~0ull;
+    tslot[0] = (uint32_t)min(t, (uint64_t)0xffffffffu);
+  }
+  __syncthreads();
+  gnext = tslot[0];
+  taken += gnext < ngroups;
+  uint32_t it = 1;
+  for (; g < ngroups; ++it) {
+    SCAN_STAMP(t0);
+    const uint64_t strip = g * kScanThreads + threadIdx.x;
+    const StripJob cur = job;
+    const uint64_t next = gnext < ngroups ? gnext * kScanThreads + threadIdx.x : ~0ull;
+    if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
+    uint64_t tk = ~0ull;
+    if (threadIdx.x == 0 && gnext < ngroups && taken < max_groups)
+      tk = gridDim.x + atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->scan_ticket), 1ull);
+#else
   for (; g * kScanThreads < a.nstrips; g += gridDim.x) {
     SCAN_STAMP(t0);
     const uint64_t strip = g * kScanThreads + threadIdx.x;
     const StripJob cur = job;
     const uint64_t next = strip + (uint64_t)gridDim.x * kScanThreads;
     if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
+#endif
     SCAN_STAMP(t1);
     bool flag = false;
     uint32_t hits = 0;
@@ -675,6 +717,13 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
     if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, cur, &hits, &t2);
     SCAN_STAMP(t3);
     refine_append(a, flag, strip, hits, lds_cnt);
+#if BSG_SCAN_DYN
+    if (threadIdx.x == 0) tslot[it & 1u] = (uint32_t)min(tk, (uint64_t)0xffffffffu);
+    __syncthreads();
+    g = gnext;
+    gnext = g < ngroups ? tslot[it & 1u] : ~0ull;
+    taken += gnext < ngroups;
+#endif
     SCAN_STAMP(t4);
 #ifdef BSG_SCAN_DIAG
     d_job += t1 - t0;
@@ -1314,6 +1363,9 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
 #ifndef BSG_LANE_LEAD
 #define BSG_LANE_LEAD 4  // iterations before a job's end at which its successor is popped
 #endif
+#ifndef BSG_LANE_ASM
+#define BSG_LANE_ASM 1   // per-lane compressions as the aligned asm statement (sha256_device.h);
+#endif                   // 0: hipcc's schedule of sha256_compress (k_sha 13.44 vs 13.10 ms, configs[2])
 #ifndef BSG_LANE_BPI
 #define BSG_LANE_BPI 2   // blocks per per-lane iteration: the job-switch and queue logic runs
 #endif                   // once per this many compressions
@@ -1697,7 +1749,13 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
                take ? ld_len : jb.L, rb[b]);
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)
-      if (act && blk + b < jb.nblocks) sha256_compress(st, W[b]);
+      if (act && blk + b < jb.nblocks) {
+#if BSG_LANE_ASM
+        sha256_compress_aligned(st, W[b]);
+#else
+        sha256_compress(st, W[b]);
+#endif
+      }
     blk += kBPI;
     if (act && blk >= jb.nblocks) {
       act = false;
@@ -2754,7 +2812,11 @@ __global__ __launch_bounds__(256) void k_sha_blobs(BlobShaArgs a) {
         }
       }
       raw_load(jb.dbase, 64ull * (blk + 1), 0, jb.L, rb);
+#if BSG_LANE_ASM
+      sha256_compress_aligned(st, W);
+#else
       sha256_compress(st, W);
+#endif
     }
     uint32_t* ref = reinterpret_cast<uint32_t*>(a.refs + 32 * i);
 #pragma unroll
@@ -2802,12 +2864,14 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
 #endif
 uint32_t scan_lists(uint64_t nstrips, int num_cus) {
   const uint64_t groups = (nstrips + kScanThreads - 1) / kScanThreads;
-  return grid_for(groups, 1, (uint32_t)BSG_SCAN_GRID * (kScanPair ? 2u : 1u) * (uint32_t)num_cus);
+  const uint32_t per_cu = BSG_SCAN_DYN ? 1u : (uint32_t)BSG_SCAN_GRID;
+  return grid_for(groups, 1, per_cu * (kScanPair ? 2u : 1u) * (uint32_t)num_cus);
 }
 
 uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists) {
   const uint64_t groups = (nstrips + kScanThreads - 1) / kScanThreads;
-  return lists ? (groups + lists - 1) / lists * (uint64_t)kScanThreads : 0;
+  const uint64_t share = lists ? (groups + lists - 1) / lists : 0;
+  return (BSG_SCAN_DYN ? min(groups, kScanDynShare * share) : share) * (uint64_t)kScanThreads;
 }
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {

@@ -94,6 +94,28 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&W)
 }
 
 
+// The same compression as one generated asm statement (tools/gen_lane_asm.py): every
+// instruction 8 bytes and 8-byte aligned. hipcc's own schedule of sha256_compress mixes 4- and
+// 8-byte encodings with about half its 8-byte instructions at 4 mod 8, and takes 235 VGPRs in
+// k_sha against 188 with this one. A lone wave runs both at ~6,000 cycles per block
+// (profiles/r05_lanes_align.log); in k_sha under the configs[2] load the asm form takes k_sha
+// from 13.44 to 13.10 ms (profiles/r05_ab8.log). k_sha's per-lane mode uses it (BSG_LANE_ASM).
+#include "sha256_lane_asm.inc"
+__device__ __forceinline__ void sha256_compress_aligned(uint32_t (&st)[8], uint32_t (&W)[16]) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7, t0, t1, t2, t3, t4, t5, k;
+  asm volatile(BSG_LANE_COMPRESS_ASM
+               : [st0] "+v"(st[0]), [st1] "+v"(st[1]), [st2] "+v"(st[2]), [st3] "+v"(st[3]),
+                 [st4] "+v"(st[4]), [st5] "+v"(st[5]), [st6] "+v"(st[6]), [st7] "+v"(st[7]),
+                 [w0] "+v"(W[0]), [w1] "+v"(W[1]), [w2] "+v"(W[2]), [w3] "+v"(W[3]),
+                 [w4] "+v"(W[4]), [w5] "+v"(W[5]), [w6] "+v"(W[6]), [w7] "+v"(W[7]),
+                 [w8] "+v"(W[8]), [w9] "+v"(W[9]), [w10] "+v"(W[10]), [w11] "+v"(W[11]),
+                 [w12] "+v"(W[12]), [w13] "+v"(W[13]), [w14] "+v"(W[14]), [w15] "+v"(W[15]),
+                 [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3),
+                 [x4] "=&v"(x4), [x5] "=&v"(x5), [x6] "=&v"(x6), [x7] "=&v"(x7),
+                 [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+                 [t4] "=&v"(t4), [t5] "=&v"(t5), [k] "=&s"(k));
+}
+
 // Variant for experiments (tools/ubench): plain C operators, left to hipcc's selection.
 #define SHA_ROUND_C(a, b, c, d, e, f, g, h, kw)                               \
   do {                                                                         \
