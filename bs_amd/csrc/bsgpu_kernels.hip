@@ -298,8 +298,9 @@ __device__ __forceinline__ void hit_mark(uint32_t (&hits)[N], uint32_t b, bool h
 constexpr int kHitWords = (kStrip / 64 + 31) / 32;
 static_assert(kHitWords == 1, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
 
-template <bool WIDE, bool PRE>
-__device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
+// NH hit words: 1 for one strip, 2 for a lane's span of two strips (BSG_SCAN_PAIR).
+template <bool WIDE, bool PRE, int NH>
+__device__ __forceinline__ uint64_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
                                                      uint32_t lane4, const uint8_t* base,
                                                      uint32_t nfull, uint32_t& h,
                                                      uint32_t (&hA)[64], uint32_t (&w0)[16],
@@ -310,7 +311,7 @@ __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const ui
   // the line is fetched once: loaded one block apart, the second half often found its line
   // evicted from L2 and fetched it again (k_scan read 1.5x its input on configs[1]).
   uint32_t n0[16], n1[16];
-  uint32_t hits[1] = {0};
+  uint32_t hits[NH] = {};
   if (!PRE) {  // (PRE: the caller loaded blocks 0 and 1 beside the history block)
     scan_load16(base, w0);
     scan_load16(base + 64ull * min(1u, nfull - 1), w1);  // (clamped, branch-free)
@@ -335,7 +336,8 @@ __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const ui
 #pragma unroll
     for (int k = 0; k < 64; ++k) hA[k] = hB[k];
   }
-  return hits[0];
+  if constexpr (NH == 1) return hits[0];
+  else return ((uint64_t)hits[1] << 32) | hits[0];
 }
 
 // strip0 (the streams' first strips) cached in LDS after the table, when it fits: the stream
@@ -386,6 +388,8 @@ struct StripJob {
   uint64_t start;      // segment offset of the strip
   uint32_t len;        // bytes in the strip
   bool tail;           // k_refine has the segment's < 64-byte tail or the final flush here
+  bool fin;            // the segment ends its stream (Splitter.Close's flush at its last byte)
+  uint64_t seglen;     // the segment's length
 };
 
 __device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip, lds_u64p s0) {
@@ -397,6 +401,8 @@ __device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip,
   j.start = l.start;
   j.len = l.len;
   j.tail = (l.len & 63u) != 0 || (l.last && sd->finalize);
+  j.fin = sd->finalize;
+  j.seglen = sd->len;
   return j;
 }
 
@@ -439,6 +445,8 @@ __device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip,
   j.d = a.data + data_off;
   j.pre = j.start >= 64 ? j.d + j.start - 64 : a.streams[s].hist;  // an address, not a load
   j.tail = (j.len & 63u) != 0 || (j.start + j.len == seglen && (len_fin & kLenFin) != 0);
+  j.fin = (len_fin & kLenFin) != 0;
+  j.seglen = seglen;
   return j;
 }
 
@@ -469,13 +477,24 @@ __device__ __forceinline__ uint32_t fold64(const uint32_t (&t)[64]) {
 #ifndef BSG_SCAN_WARM
 #define BSG_SCAN_WARM 0  // 1: the history's lookups all issued, then folded by fold64 (round 5
 #endif                   // experiment); 0: the running form h = rotl1(h) ^ t
+// Fast pass over len bytes from a strip's start (one strip, or BSG_SCAN_PAIR's two contiguous
+// strips of one segment): the rolling hash at every position of the full 64-byte blocks, a hit
+// bit per block whose pre-filter fires (bit b: block b from the first strip's start).
+// BSG_SCAN_PAIR=1 (experiment): a lane scans two contiguous strips as one span, the second
+// without a warm-up. It cut k_scan's HBM reads from 1.069x to 1.037x of the input on configs[2]
+// (1.100x -> 1.059x on configs[1]: the history line of every strip came from HBM twice) but the
+// line loop ran 17 % slower per byte with lanes 4 KiB apart instead of 2 (same loop code), and
+// configs[1] k_scan went from 0.27 to 0.34 ms (profiles/r05_ab14_*.log, r05_scan_stamps14_pair.log).
+#ifndef BSG_SCAN_PAIR
+#define BSG_SCAN_PAIR 0
+#endif
 template <bool WIDE>
-__device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* tab, uint32_t lane4,
-                                           uint64_t strip, const StripJob& j, uint32_t* hits_out,
-                                           uint64_t* t_warm) {
+__device__ __forceinline__ uint64_t scan_span(const ScanArgs& a, const uint32_t* tab,
+                                              uint32_t lane4, const StripJob& j, uint32_t len,
+                                              uint64_t* t_warm) {
   uint32_t w[16];
   load16(j.pre, w);
-  const uint32_t nfull = j.len >> 6;
+  const uint32_t nfull = len >> 6;
   uint32_t w0[16], w1[16];
 #if BSG_SCAN_LOAD3
   // the strip's first line in flight with its history block: one HBM round trip per strip start
@@ -503,13 +522,11 @@ __device__ __forceinline__ bool scan_strip(const ScanArgs& a, const uint32_t* ta
 #else
   (void)t_warm;
 #endif
-  uint32_t hits = 0;
+  uint64_t hits = 0;
   if (nfull)
-    hits = scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0>(a, tab, lane4, j.d + j.start, nfull, h,
-                                                       hist, w0, w1);
-  a.counts[strip] = 0u;
-  *hits_out = hits;
-  return hits || j.tail;
+    hits = scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0, BSG_SCAN_PAIR ? 2 : 1>(
+        a, tab, lane4, j.d + j.start, nfull, h, hist, w0, w1);
+  return hits;
 }
 
 #ifndef BSG_SCAN_FUSE
@@ -636,6 +653,8 @@ constexpr uint64_t kScanDynShare = 2;
 constexpr uint32_t kScanThreads = BSG_SCAN_WGS;
 static_assert(kScanThreads == 512 || kScanThreads == 256, "k_scan workgroup size");
 constexpr bool kScanPair = kScanThreads == 256;  // two workgroups per CU
+constexpr uint32_t kScanSpan = BSG_SCAN_PAIR ? 2u : 1u;    // strips per lane per iteration
+constexpr uint32_t kScanGroup = kScanThreads * kScanSpan;  // strips per workgroup iteration
 constexpr uint32_t kScanStrip0Cap = kScanPair ? kStrip0Lds - 2 : kStrip0Lds;
 constexpr uint32_t kScanLdsStrip0 = kTabRows * kTabRep * 4;
 constexpr uint32_t kScanLdsStreams = kScanLdsStrip0 + kScanStrip0Cap * 8;
@@ -671,15 +690,15 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   uint64_t g = blockIdx.x;
   StripJob job{};
-  if (g * kScanThreads + threadIdx.x < a.nstrips)
-    job = strip_job(a, g * kScanThreads + threadIdx.x, s0, sc);
+  if (g * kScanGroup + kScanSpan * threadIdx.x < a.nstrips)
+    job = strip_job(a, g * kScanGroup + kScanSpan * threadIdx.x, s0, sc);
 #if BSG_SCAN_DYN
   // group tickets: the first group is blockIdx.x, later ones gridDim.x + the counter's value.
   // Thread 0 takes the ticket after next while the current group is scanned; it reaches the
   // others through LDS slot (iteration & 1) behind the iteration's barrier (a slot is written
   // again two iterations later, after every thread has passed the barrier that follows its reads).
-  const uint64_t ngroups = (a.nstrips + kScanThreads - 1) / kScanThreads;
-  const uint64_t max_groups = a.list_cap / kScanThreads;  // the refine list's bound
+  const uint64_t ngroups = (a.nstrips + kScanGroup - 1) / kScanGroup;
+  const uint64_t max_groups = a.list_cap / kScanGroup;  // the refine list's bound
   uint32_t* tslot = lds_cnt + 1;
   uint64_t taken = 1;
   uint64_t gnext = ~0ull;
@@ -695,28 +714,79 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   uint32_t it = 1;
   for (; g < ngroups; ++it) {
     SCAN_STAMP(t0);
-    const uint64_t strip = g * kScanThreads + threadIdx.x;
+    const uint64_t strip = g * kScanGroup + kScanSpan * threadIdx.x;
     const StripJob cur = job;
-    const uint64_t next = gnext < ngroups ? gnext * kScanThreads + threadIdx.x : ~0ull;
+    const uint64_t next = gnext < ngroups ? gnext * kScanGroup + kScanSpan * threadIdx.x : ~0ull;
     if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
     uint64_t tk = ~0ull;
     if (threadIdx.x == 0 && gnext < ngroups && taken < max_groups)
       tk = gridDim.x + atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->scan_ticket), 1ull);
 #else
-  for (; g * kScanThreads < a.nstrips; g += gridDim.x) {
+  for (; g * kScanGroup < a.nstrips; g += gridDim.x) {
     SCAN_STAMP(t0);
-    const uint64_t strip = g * kScanThreads + threadIdx.x;
+    const uint64_t strip = g * kScanGroup + kScanSpan * threadIdx.x;
     const StripJob cur = job;
-    const uint64_t next = strip + (uint64_t)gridDim.x * kScanThreads;
+    const uint64_t next = strip + (uint64_t)gridDim.x * kScanGroup;
     if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
 #endif
     SCAN_STAMP(t1);
+    uint64_t t2 = 0;  // (BSG_SCAN_DIAG: the end of the history's warm-up)
+#if BSG_SCAN_PAIR
+    // strips 2i and 2i+1 of the group: one span when they are contiguous in one segment (the
+    // second needs no warm-up, and its history line is not fetched a second time: the first
+    // strip's last line, read ~45 us apart by two lanes, came from HBM twice, 6 % of k_scan's
+    // bytes); a second pass for the strip after a segment's last one (divergent, rare)
+    bool flag_a = false, flag_b = false;
+    uint32_t hits_a = 0, hits_b = 0;
+    {
+      uint64_t sp = strip;
+      StripJob j = cur;
+      bool go = sp < a.nstrips;
+      for (int pass = 0; pass < 2; ++pass) {
+        bool merged = false;
+        if (go) {
+          merged = pass == 0 && sp + 1 < a.nstrips && j.start + j.len < j.seglen;
+          const uint32_t len_b =
+              merged ? (uint32_t)min((uint64_t)kStrip, j.seglen - j.start - kStrip) : 0u;
+          const uint64_t m = scan_span<WIDE>(a, tab, lane4, j, j.len + len_b, &t2);
+          const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+          a.counts[sp] = 0u;
+          if (pass == 0) {
+            hits_a = lo;
+            flag_a = lo || j.tail;  // (a merged first strip is full and not its segment's last)
+            if (merged) {
+              a.counts[sp + 1] = 0u;
+              const uint64_t end_b = j.start + kStrip + len_b;
+              hits_b = hi;
+              flag_b = hi || (len_b & 63u) || (end_b == j.seglen && j.fin);
+            }
+          } else {
+            hits_b = lo;
+            flag_b = lo || j.tail;
+          }
+        }
+        go = go && pass == 0 && !merged && sp + 1 < a.nstrips;
+        if (!__ballot(go)) break;
+        if (go) {
+          sp += 1;
+          j = strip_job(a, sp, s0, sc);
+        }
+      }
+    }
+    SCAN_STAMP(t3);
+    refine_append(a, flag_a, strip, hits_a, lds_cnt);
+    refine_append(a, flag_b, strip + 1, hits_b, lds_cnt);
+#else
     bool flag = false;
     uint32_t hits = 0;
-    uint64_t t2 = 0;  // (BSG_SCAN_DIAG: the end of the history's warm-up)
-    if (strip < a.nstrips) flag = scan_strip<WIDE>(a, tab, lane4, strip, cur, &hits, &t2);
+    if (strip < a.nstrips) {
+      hits = (uint32_t)scan_span<WIDE>(a, tab, lane4, cur, cur.len, &t2);
+      a.counts[strip] = 0u;
+      flag = hits || cur.tail;
+    }
     SCAN_STAMP(t3);
     refine_append(a, flag, strip, hits, lds_cnt);
+#endif
 #if BSG_SCAN_DYN
     if (threadIdx.x == 0) tslot[it & 1u] = (uint32_t)min(tk, (uint64_t)0xffffffffu);
     __syncthreads();
@@ -2863,15 +2933,15 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
 #define BSG_SCAN_GRID 2  // k_scan workgroups per CU in the grid (one is resident at a time)
 #endif
 uint32_t scan_lists(uint64_t nstrips, int num_cus) {
-  const uint64_t groups = (nstrips + kScanThreads - 1) / kScanThreads;
+  const uint64_t groups = (nstrips + kScanGroup - 1) / kScanGroup;
   const uint32_t per_cu = BSG_SCAN_DYN ? 1u : (uint32_t)BSG_SCAN_GRID;
   return grid_for(groups, 1, per_cu * (kScanPair ? 2u : 1u) * (uint32_t)num_cus);
 }
 
 uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists) {
-  const uint64_t groups = (nstrips + kScanThreads - 1) / kScanThreads;
+  const uint64_t groups = (nstrips + kScanGroup - 1) / kScanGroup;
   const uint64_t share = lists ? (groups + lists - 1) / lists : 0;
-  return (BSG_SCAN_DYN ? min(groups, kScanDynShare * share) : share) * (uint64_t)kScanThreads;
+  return (BSG_SCAN_DYN ? min(groups, kScanDynShare * share) : share) * (uint64_t)kScanGroup;
 }
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {

@@ -16,6 +16,11 @@ also calibrated on its own: tools/ubench/scan_calib reads a known byte count wit
 pattern (k_strips) and with the guide's coalesced pattern (k_coalesced); --calib <dir> reads
 that run's FETCH_SIZE pass and reports, per kernel of the strip pattern, its FETCH per
 algorithmic byte relative to k_strips'. WRITE_SIZE is exact for 16-B streaming stores.
+
+--rdreq <dir> (round 5): a pass of TCC_EA0_RDREQ split by request size (32/64/128-B,
+tools/rdreq_summary.py) gives the read bytes directly (32 x n32 + 64 x n64 + 128 x n128; the
+coalesced calibration kernel reads exactly its 1 GiB this way); when given, it replaces the
+FETCH_SIZE read bytes of every kernel it saw, and FETCH_SIZE stays in the file as a cross-check.
 """
 import argparse
 import collections
@@ -49,7 +54,14 @@ def main():
     ap.add_argument("--bytes", type=float, default=float(1 << 30),
                     help="algorithmic input bytes per launch (stream bytes of the batch)")
     ap.add_argument("--calib", default=None, help="scan_calib FETCH_SIZE run directory")
+    ap.add_argument("--rdreq", default=None, help="TCC_EA0_RDREQ-by-size run directory")
     a = ap.parse_args()
+    rdreq = None
+    if a.rdreq:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from rdreq_summary import summarise
+        rdreq = summarise(a.rdreq, a.bytes)
     calib = None
     if a.calib:
         cf = _counters(os.path.join(a.calib, "run_counter_collection.csv"))
@@ -76,10 +88,15 @@ def main():
         x2 = name in FETCH_X2
         fb = fk * 1024 * (2 if x2 else 1)
         wb = wk * 1024
+        corr = "x2 (16 B/lane reads, gfx950)" if x2 else "uncalibrated (raw)"
+        if rdreq and name in rdreq:
+            fb_fetch = fb
+            fb = rdreq[name]["read_bytes_per_launch"]
+            corr = f"TCC_EA0_RDREQ by request size (FETCH_SIZE-based: {fb_fetch:.0f} B)"
         kernels[name] = {
             "launches": len(fetch.get(name, [])),
             "fetch_kib_raw": fk, "write_kib_raw": wk,
-            "fetch_correction": "x2 (16 B/lane reads, gfx950)" if x2 else "uncalibrated (raw)",
+            "fetch_correction": corr,
             "hbm_bytes_per_launch": fb + wb,
             "read_over_algorithmic": fb / a.bytes,
             "write_bytes_per_launch": wb,
@@ -90,7 +107,9 @@ def main():
                 calib["k_strips_fetch_per_byte"]
     doc = {"round": a.round, "workload": a.workload, "algorithmic_bytes_per_launch": a.bytes,
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py "
-                     "--steps 1 --warmup 0", "strip_pattern_calibration": calib,
+                     "--steps 1 --warmup 0" + ("; reads from a TCC_EA0_RDREQ_{32B,64B,128B} pass"
+                                               if rdreq else ""),
+           "strip_pattern_calibration": calib,
            "kernels": kernels}
     with open(os.path.join(out, f"{a.round}_pmc.json"), "w") as f:
         json.dump(doc, f, indent=1)
