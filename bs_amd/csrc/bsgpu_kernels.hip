@@ -1434,8 +1434,9 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
 #define BSG_LANE_LEAD 4  // iterations before a job's end at which its successor is popped
 #endif
 #ifndef BSG_LANE_ASM
-#define BSG_LANE_ASM 1   // per-lane compressions as the aligned asm statement (sha256_device.h);
-#endif                   // 0: hipcc's schedule of sha256_compress (k_sha 13.44 vs 13.10 ms, configs[2])
+#define BSG_LANE_ASM 2   // per-lane compressions as the aligned asm statement (sha256_device.h):
+#endif                   // 2 with K in 64 resident VGPRs, 1 with K through an SGPR; 0: hipcc's
+                         // schedule of sha256_compress (k_sha 13.44 vs 13.10 ms at 1, configs[2])
 #ifndef BSG_LANE_BPI
 #define BSG_LANE_BPI 2   // blocks per per-lane iteration: the job-switch and queue logic runs
 #endif                   // once per this many compressions
@@ -1668,6 +1669,10 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
   jb.nblocks = 0;
   jb.fin = 1;
   uint32_t st[8] = {};
+#if BSG_LANE_ASM == 2
+  uint32_t kv[64];  // K, resident for the whole loop (k_sha has one wave per SIMD: VGPRs to spare)
+  sha256_k_regs(kv);
+#endif
   RawBlock rb[kBPI];
 #pragma unroll
   for (int b = 0; b < kBPI; ++b) {
@@ -1820,7 +1825,9 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)
       if (act && blk + b < jb.nblocks) {
-#if BSG_LANE_ASM
+#if BSG_LANE_ASM == 2
+        sha256_compress_kv(st, W[b], kv);
+#elif BSG_LANE_ASM
         sha256_compress_aligned(st, W[b]);
 #else
         sha256_compress(st, W[b]);

@@ -116,6 +116,47 @@ __device__ __forceinline__ void sha256_compress_aligned(uint32_t (&st)[8], uint3
                  [t4] "=&v"(t4), [t5] "=&v"(t5), [k] "=&s"(k));
 }
 
+// The same with K from 64 VGPRs the caller keeps resident (sha256_k_regs): no s_mov per round,
+// for a wave that runs alone on its SIMD and issues every instruction at ~4 cycles, VALU or
+// not (k_sha's per-lane mode: 5,782 against 5,979 cycles per block, tools/ubench/lanes_align.hip,
+// profiles/r05_lanes_v4.log).
+__device__ __forceinline__ void sha256_k_regs(uint32_t (&kv)[64]) {
+#pragma unroll
+  for (int i = 0; i < 64; ++i)  // opaque moves: the values stay in registers, not rematerialised
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kv[i]) : "i"(kK256[i]));
+}
+__device__ __forceinline__ void sha256_compress_kv(uint32_t (&st)[8], uint32_t (&W)[16],
+                                                   const uint32_t (&kv)[64]) {
+  uint32_t x0, x1, x2, x3, x4, x5, x6, x7, t0, t1, t2, t3, t4, t5;
+  asm volatile(BSG_LANE_COMPRESS_ASM_KV
+               : [st0] "+v"(st[0]), [st1] "+v"(st[1]), [st2] "+v"(st[2]), [st3] "+v"(st[3]),
+                 [st4] "+v"(st[4]), [st5] "+v"(st[5]), [st6] "+v"(st[6]), [st7] "+v"(st[7]),
+                 [w0] "+v"(W[0]), [w1] "+v"(W[1]), [w2] "+v"(W[2]), [w3] "+v"(W[3]),
+                 [w4] "+v"(W[4]), [w5] "+v"(W[5]), [w6] "+v"(W[6]), [w7] "+v"(W[7]),
+                 [w8] "+v"(W[8]), [w9] "+v"(W[9]), [w10] "+v"(W[10]), [w11] "+v"(W[11]),
+                 [w12] "+v"(W[12]), [w13] "+v"(W[13]), [w14] "+v"(W[14]), [w15] "+v"(W[15]),
+                 [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2), [x3] "=&v"(x3),
+                 [x4] "=&v"(x4), [x5] "=&v"(x5), [x6] "=&v"(x6), [x7] "=&v"(x7),
+                 [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),
+                 [t4] "=&v"(t4), [t5] "=&v"(t5)
+               : [k0] "v"(kv[0]), [k1] "v"(kv[1]), [k2] "v"(kv[2]), [k3] "v"(kv[3]),
+                 [k4] "v"(kv[4]), [k5] "v"(kv[5]), [k6] "v"(kv[6]), [k7] "v"(kv[7]),
+                 [k8] "v"(kv[8]), [k9] "v"(kv[9]), [k10] "v"(kv[10]), [k11] "v"(kv[11]),
+                 [k12] "v"(kv[12]), [k13] "v"(kv[13]), [k14] "v"(kv[14]), [k15] "v"(kv[15]),
+                 [k16] "v"(kv[16]), [k17] "v"(kv[17]), [k18] "v"(kv[18]), [k19] "v"(kv[19]),
+                 [k20] "v"(kv[20]), [k21] "v"(kv[21]), [k22] "v"(kv[22]), [k23] "v"(kv[23]),
+                 [k24] "v"(kv[24]), [k25] "v"(kv[25]), [k26] "v"(kv[26]), [k27] "v"(kv[27]),
+                 [k28] "v"(kv[28]), [k29] "v"(kv[29]), [k30] "v"(kv[30]), [k31] "v"(kv[31]),
+                 [k32] "v"(kv[32]), [k33] "v"(kv[33]), [k34] "v"(kv[34]), [k35] "v"(kv[35]),
+                 [k36] "v"(kv[36]), [k37] "v"(kv[37]), [k38] "v"(kv[38]), [k39] "v"(kv[39]),
+                 [k40] "v"(kv[40]), [k41] "v"(kv[41]), [k42] "v"(kv[42]), [k43] "v"(kv[43]),
+                 [k44] "v"(kv[44]), [k45] "v"(kv[45]), [k46] "v"(kv[46]), [k47] "v"(kv[47]),
+                 [k48] "v"(kv[48]), [k49] "v"(kv[49]), [k50] "v"(kv[50]), [k51] "v"(kv[51]),
+                 [k52] "v"(kv[52]), [k53] "v"(kv[53]), [k54] "v"(kv[54]), [k55] "v"(kv[55]),
+                 [k56] "v"(kv[56]), [k57] "v"(kv[57]), [k58] "v"(kv[58]), [k59] "v"(kv[59]),
+                 [k60] "v"(kv[60]), [k61] "v"(kv[61]), [k62] "v"(kv[62]), [k63] "v"(kv[63]));
+}
+
 // Variant for experiments (tools/ubench): plain C operators, left to hipcc's selection.
 #define SHA_ROUND_C(a, b, c, d, e, f, g, h, kw)                               \
   do {                                                                         \

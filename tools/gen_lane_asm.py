@@ -4,8 +4,9 @@ inline-asm statement, every instruction 8 bytes (VOP3, or VOP2 + a 32-bit litera
 and the statement 8-byte aligned (.p2align 3), so no 8-byte instruction starts at 4 mod 8: the
 round-5 octet measurements (tools/gen_oct_variants.py, profiles/r05_oct_var_alignment.log) cost
 each such instruction ~10 cycles of a lone wave, and k_sha's per-lane waves run one per SIMD.
-Writes bs_amd/csrc/sha256_lane_asm.inc (BSG_LANE_COMPRESS_ASM; operands st0..st7, w0..w15
-read-write, t0..t5 scratch)."""
+Writes bs_amd/csrc/sha256_lane_asm.inc: BSG_LANE_COMPRESS_ASM (operands st0..st7, w0..w15
+read-write, x0..x7, t0..t5 and the SGPR k scratch) and BSG_LANE_COMPRESS_ASM_KV (the same with
+K read from the VGPR inputs k0..k63 instead of the SGPR: no s_mov per round)."""
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,7 +23,7 @@ K = [0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x9
      0xc67178f2]
 
 
-def body(nomov=False, sgprk=False):
+def body(nomov=False, sgprk=False, vgprk=False):
     """The statement's instruction lines. nomov: rounds 0-3 write their new a and e into the
     x registers instead of copying st into x first (8 moves fewer); sgprk: K goes through an
     SGPR (s_mov, then one v_add3 of h, K and W) instead of a VOP2 literal add (64 VALU fewer,
@@ -67,25 +68,27 @@ def body(nomov=False, sgprk=False):
         else:
             nd, nh = names[3], names[7]
         od, oh = regs[nd], regs[nh]
-        if sgprk:
+        if sgprk and not vgprk:
             e(f"s_mov_b32 %[k], 0x{K[i]:08x}")
         e(f"v_alignbit_b32 {T[0]}, {ee}, {ee}, 6")
         e(f"v_alignbit_b32 {T[1]}, {ee}, {ee}, 11")
         e(f"v_alignbit_b32 {T[2]}, {ee}, {ee}, 25")
         e(f"v_bitop3_b32 {T[4]}, {ee}, {f}, {g} bitop3:0xca")
-        if sgprk:
+        if vgprk:
+            e(f"v_add3_u32 {T[5]}, {h}, %[k{i}], {W[i & 15]}")
+        elif sgprk:
             e(f"v_add3_u32 {T[5]}, {h}, %[k], {W[i & 15]}")
         else:
             e(f"v_add_u32_e32 {T[5]}, 0x{K[i]:08x}, {W[i & 15]}")
         e(f"v_bitop3_b32 {T[0]}, {T[0]}, {T[1]}, {T[2]} bitop3:0x96")
         e(f"v_alignbit_b32 {T[1]}, {a}, {a}, 2")
         e(f"v_alignbit_b32 {T[2]}, {a}, {a}, 13")
-        if sgprk:
+        if sgprk or vgprk:
             e(f"v_add3_u32 {T[5]}, {T[5]}, {T[0]}, {T[4]}")
         else:
             e(f"v_add3_u32 {T[5]}, {h}, {T[5]}, {T[0]}")
         e(f"v_alignbit_b32 {T[3]}, {a}, {a}, 22")
-        if not sgprk:
+        if not (sgprk or vgprk):
             e(f"v_add_u32_e64 {T[5]}, {T[5]}, {T[4]}")
         e(f"v_bitop3_b32 {T[4]}, {a}, {b}, {c} bitop3:0xe8")
         e(f"v_bitop3_b32 {T[1]}, {T[1]}, {T[2]}, {T[3]} bitop3:0x96")
@@ -106,16 +109,19 @@ def macro(name, lines, n_valu, what):
 
 def gen():
     L, n = body(nomov=True, sgprk=True)
+    L4, n4 = body(nomov=True, vgprk=True)
     with open(OUT, "w") as f:
         f.write("// GENERATED by tools/gen_lane_asm.py -- do not edit.\n")
-        f.write(macro("BSG_LANE_COMPRESS_ASM", L, n, ""))
-    print(f"wrote {OUT}: {n} VALU")
+        f.write(macro("BSG_LANE_COMPRESS_ASM", L, n, " (K through an SGPR)"))
+        f.write(macro("BSG_LANE_COMPRESS_ASM_KV", L4, n4, " (K from 64 resident VGPRs k0..k63)"))
+    print(f"wrote {OUT}: {n} / {n4} VALU")
     # the round-5 variants side by side for tools/ubench/lanes_align.hip
     out = os.path.join(ROOT, "tools", "ubench", "lane_variants.inc")
     with open(out, "w") as f:
         f.write("// GENERATED by tools/gen_lane_asm.py -- do not edit.\n")
         for nm, kw in (("LANE_V1", {}), ("LANE_V2", {"nomov": True}),
-                       ("LANE_V3", {"nomov": True, "sgprk": True})):
+                       ("LANE_V3", {"nomov": True, "sgprk": True}),
+                       ("LANE_V4", {"nomov": True, "vgprk": True})):
             L, n = body(**kw)
             f.write(macro(nm, L, n, f" ({kw})"))
             print(f"{nm} {kw}: {n} VALU")
