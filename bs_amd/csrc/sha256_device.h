@@ -391,6 +391,9 @@ __device__ __forceinline__ void sha256_blocks_skew(uint32_t (&hs)[4], const uint
                                                    uint32_t stride, uint32_t nblk, int32_t lim,
                                                    const SkewLane& b) {
   if (nblk == 0) return;
+  // wave-uniform, but under register pressure hipcc may hold it in a VGPR, which the "s"
+  // operand below does not stop (the loop's s_cmp then fails to assemble)
+  nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)nblk);
   const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) const uint32_t*)row);
   const uint64_t amask = 0xAAAAAAAAAAAAAAAAull;  // A lanes: odd
@@ -439,6 +442,9 @@ __device__ __forceinline__ void sha256_blocks_oct(uint32_t (&hs)[4], const uint3
                                                   uint32_t stride, uint32_t nblk, int32_t lim,
                                                   const OctLane& b) {
   if (nblk == 0) return;
+  // wave-uniform, but under register pressure hipcc may hold it in a VGPR, which the "s"
+  // operand below does not stop (the loop's s_cmp then fails to assemble)
+  nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)nblk);
   const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) const uint32_t*)row);
   const uint64_t amask = 0xF0F0F0F0F0F0F0F0ull;  // A lanes: octet positions 4-7
