@@ -238,7 +238,7 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     mv = memoryview(data)
     piece = 32 << 20
     w = bsgpu.StreamingSplitter(bits=bits, min_size=min_size, device=device)
-    best, nch, recs = None, 0, []
+    best, nch, recs, reps = None, 0, [], []
     for rep in range(4):  # rep 0 grows the pinned staging; best of the other three
         w.reset()
         recs = []
@@ -246,9 +246,11 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
         for i in range(0, n, piece):
             w.write(mv[i:i + piece])
             recs.append(w.drain())
+        tw = time.perf_counter() - t0
         w.close()
         recs.append(w.drain())
         dt = time.perf_counter() - t0
+        reps.append([round(dt * 1e3, 2), round(tw * 1e3, 2)])
         if rep and (best is None or dt < best):
             best = dt
     w.free()
@@ -257,6 +259,7 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     nch = len(last)
     return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "chunks": nch,
             "records": last,
+            "reps_ms": reps,  # [whole rep, of which the Write calls] per rep, rep 0 = warm-up
             "path": "host memory -> bsg_write (ring of 4 x 64 MiB pinned stages, each copied "
                     "H2D as it fills, on a copy stream into 4 device data slots) -> split + "
                     "SHA-256 on 3 engines -> records in host memory; tile 256 MiB"}
