@@ -298,7 +298,7 @@ __device__ __forceinline__ void hit_mark(uint32_t (&hits)[N], uint32_t b, bool h
 constexpr int kHitWords = (kStrip / 64 + 31) / 32;
 static_assert(kHitWords == 1, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
 
-// NH hit words: 1 for one strip, 2 for a lane's span of two strips (BSG_SCAN_PAIR).
+// NH hit words: 1 for one strip (2: the round-5 two-strip span experiment).
 template <bool WIDE, bool PRE, int NH>
 __device__ __forceinline__ uint64_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
                                                      uint32_t lane4, const uint8_t* base,
@@ -477,34 +477,41 @@ __device__ __forceinline__ uint32_t fold64(const uint32_t (&t)[64]) {
 #ifndef BSG_SCAN_WARM
 #define BSG_SCAN_WARM 0  // 1: the history's lookups all issued, then folded by fold64 (round 5
 #endif                   // experiment); 0: the running form h = rotl1(h) ^ t
-// Fast pass over len bytes from a strip's start (one strip, or BSG_SCAN_PAIR's two contiguous
-// strips of one segment): the rolling hash at every position of the full 64-byte blocks, a hit
-// bit per block whose pre-filter fires (bit b: block b from the first strip's start).
-// BSG_SCAN_PAIR=1 (experiment): a lane scans two contiguous strips as one span, the second
-// without a warm-up. It cut k_scan's HBM reads from 1.069x to 1.037x of the input on configs[2]
-// (1.100x -> 1.059x on configs[1]: the history line of every strip came from HBM twice) but the
-// line loop ran 17 % slower per byte with lanes 4 KiB apart instead of 2 (same loop code), and
-// configs[1] k_scan went from 0.27 to 0.34 ms (profiles/r05_ab14_*.log, r05_scan_stamps14_pair.log).
-#ifndef BSG_SCAN_PAIR
-#define BSG_SCAN_PAIR 0
+// Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
+// hit bit per block whose pre-filter fires.
+//
+// BSG_SCAN_CHAIN (chained strips): lane l's strip follows lane l-1's in the same segment for
+// every lane but a wave's first and a segment's first strip. Such a strip does not read the 64
+// bytes before it: it warms up on its own block 0 (the hash at its byte 63, checked), and lane
+// l-1 checks positions 0..62 of it by running its hash on past its own end, with block 0's
+// words taken from lane l by a lane shift and its hit bit handed back the same way. The history
+// block was the second half of lane l-1's last line, read by the two lanes ~45 us apart, so
+// that line came from HBM twice: 128 of every 2,048 bytes (k_scan read 1.100x / 1.069x its
+// input on configs[1] / [2], profiles/r05_rdreq_c*.json). Lanes stay 2 KiB apart: a lane
+// scanning two strips (4 KiB apart, round-5 experiment) fetched less but ran the loop 17 %
+// slower (profiles/r05_ab14_*.log).
+#ifndef BSG_SCAN_CHAIN
+#define BSG_SCAN_CHAIN 0
 #endif
 template <bool WIDE>
-__device__ __forceinline__ uint64_t scan_span(const ScanArgs& a, const uint32_t* tab,
-                                              uint32_t lane4, const StripJob& j, uint32_t len,
-                                              uint64_t* t_warm) {
-  uint32_t w[16];
-  load16(j.pre, w);
-  const uint32_t nfull = len >> 6;
+__device__ __forceinline__ uint32_t scan_span(const ScanArgs& a, const uint32_t* tab,
+                                              uint32_t lane4, const StripJob& j, bool chained,
+                                              uint32_t (&w)[16], uint32_t& h,
+                                              uint32_t (&hist)[64], uint64_t* t_warm) {
+  const uint32_t nfull = j.len >> 6;
+  const uint32_t first = chained ? 1u : 0u;  // blocks folded in by the warm-up
+  const uint32_t nloop = nfull - first;      // (chained: nfull >= 1)
+  const uint8_t* base = j.d + j.start + 64ull * first;
+  load16(chained ? j.d + j.start : j.pre, w);
   uint32_t w0[16], w1[16];
 #if BSG_SCAN_LOAD3
-  // the strip's first line in flight with its history block: one HBM round trip per strip start
-  // instead of two (a strip under 64 bytes reads within BSG_READ_SLACK)
-  scan_load16(j.d + j.start, w0);
-  scan_load16(j.d + j.start + 64ull * min(1u, nfull - 1), w1);
+  // the strip's first line in flight with the warm-up block: one HBM round trip per strip start
+  // instead of two (a short strip reads within kReadSlack)
+  scan_load16(base, w0);
+  scan_load16(base + 64ull * min(1u, nloop - 1), w1);
   __builtin_amdgcn_sched_barrier(0);
 #endif
-  uint32_t hist[64];
-  uint32_t h = 0;
+  h = 0;
 #if BSG_SCAN_WARM
 #pragma unroll
   for (int k = 0; k < 64; ++k) hist[k] = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
@@ -522,10 +529,11 @@ __device__ __forceinline__ uint64_t scan_span(const ScanArgs& a, const uint32_t*
 #else
   (void)t_warm;
 #endif
-  uint64_t hits = 0;
-  if (nfull)
-    hits = scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0, BSG_SCAN_PAIR ? 2 : 1>(
-        a, tab, lane4, j.d + j.start, nfull, h, hist, w0, w1);
+  // chained: block 0's last position, the one its window holds whole
+  uint32_t hits = (chained && (h & (WIDE ? 0xffffu : a.p.mask)) == 0) ? 1u : 0u;
+  if (nloop)
+    hits |= (uint32_t)scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0, 1>(a, tab, lane4, base, nloop,
+                                                                     h, hist, w0, w1) << first;
   return hits;
 }
 
@@ -653,7 +661,7 @@ constexpr uint64_t kScanDynShare = 2;
 constexpr uint32_t kScanThreads = BSG_SCAN_WGS;
 static_assert(kScanThreads == 512 || kScanThreads == 256, "k_scan workgroup size");
 constexpr bool kScanPair = kScanThreads == 256;  // two workgroups per CU
-constexpr uint32_t kScanSpan = BSG_SCAN_PAIR ? 2u : 1u;    // strips per lane per iteration
+constexpr uint32_t kScanSpan = 1u;                         // strips per lane per iteration
 constexpr uint32_t kScanGroup = kScanThreads * kScanSpan;  // strips per workgroup iteration
 constexpr uint32_t kScanStrip0Cap = kScanPair ? kStrip0Lds - 2 : kStrip0Lds;
 constexpr uint32_t kScanLdsStrip0 = kTabRows * kTabRep * 4;
@@ -731,62 +739,39 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
 #endif
     SCAN_STAMP(t1);
     uint64_t t2 = 0;  // (BSG_SCAN_DIAG: the end of the history's warm-up)
-#if BSG_SCAN_PAIR
-    // strips 2i and 2i+1 of the group: one span when they are contiguous in one segment (the
-    // second needs no warm-up, and its history line is not fetched a second time: the first
-    // strip's last line, read ~45 us apart by two lanes, came from HBM twice, 6 % of k_scan's
-    // bytes); a second pass for the strip after a segment's last one (divergent, rare)
-    bool flag_a = false, flag_b = false;
-    uint32_t hits_a = 0, hits_b = 0;
-    {
-      uint64_t sp = strip;
-      StripJob j = cur;
-      bool go = sp < a.nstrips;
-      for (int pass = 0; pass < 2; ++pass) {
-        bool merged = false;
-        if (go) {
-          merged = pass == 0 && sp + 1 < a.nstrips && j.start + j.len < j.seglen;
-          const uint32_t len_b =
-              merged ? (uint32_t)min((uint64_t)kStrip, j.seglen - j.start - kStrip) : 0u;
-          const uint64_t m = scan_span<WIDE>(a, tab, lane4, j, j.len + len_b, &t2);
-          const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-          a.counts[sp] = 0u;
-          if (pass == 0) {
-            hits_a = lo;
-            flag_a = lo || j.tail;  // (a merged first strip is full and not its segment's last)
-            if (merged) {
-              a.counts[sp + 1] = 0u;
-              const uint64_t end_b = j.start + kStrip + len_b;
-              hits_b = hi;
-              flag_b = hi || (len_b & 63u) || (end_b == j.seglen && j.fin);
-            }
-          } else {
-            hits_b = lo;
-            flag_b = lo || j.tail;
-          }
-        }
-        go = go && pass == 0 && !merged && sp + 1 < a.nstrips;
-        if (!__ballot(go)) break;
-        if (go) {
-          sp += 1;
-          j = strip_job(a, sp, s0, sc);
-        }
-      }
-    }
-    SCAN_STAMP(t3);
-    refine_append(a, flag_a, strip, hits_a, lds_cnt);
-    refine_append(a, flag_b, strip + 1, hits_b, lds_cnt);
-#else
     bool flag = false;
     uint32_t hits = 0;
-    if (strip < a.nstrips) {
-      hits = (uint32_t)scan_span<WIDE>(a, tab, lane4, cur, cur.len, &t2);
+    const bool in = strip < a.nstrips;
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool chained = BSG_SCAN_CHAIN && in && lane != 0 && cur.start != 0 && cur.len >= 64;
+    uint32_t w[16], hist[64], h = 0;
+    if (in) hits = scan_span<WIDE>(a, tab, lane4, cur, chained, w, h, hist, &t2);
+#if BSG_SCAN_CHAIN
+    {
+      // positions 0..62 of lane l+1's strip, when it is chained to this one: its block 0 by a
+      // lane shift (every lane takes part), the check on the lanes whose successor is chained
+      const uint64_t cm = __ballot(chained);
+      const bool succ = lane < 63 && ((cm >> (lane + 1)) & 1ull);
+      uint32_t ws[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ws[i] = (uint32_t)__shfl_down((int)w[i], 1);
+      bool hit_s = false;
+      if (succ) {  // (this strip is full: no tail, hist = its last block's table values)
+        uint32_t hn[64];
+        lookup64(tab, ws, hn, lane4);
+        uint32_t hh = h;
+        hit_s = chain64<WIDE, false>(tab, ws, hist, hn, hh, lane4, a.p.mask);
+      }
+      const bool from_pred = __shfl_up((int)hit_s, 1) != 0;
+      if (chained && from_pred) hits |= 1u;
+    }
+#endif
+    if (in) {
       a.counts[strip] = 0u;
       flag = hits || cur.tail;
     }
     SCAN_STAMP(t3);
     refine_append(a, flag, strip, hits, lds_cnt);
-#endif
 #if BSG_SCAN_DYN
     if (threadIdx.x == 0) tslot[it & 1u] = (uint32_t)min(tk, (uint64_t)0xffffffffu);
     __syncthreads();
