@@ -490,6 +490,10 @@ __device__ __forceinline__ uint32_t fold64(const uint32_t (&t)[64]) {
 // input on configs[1] / [2], profiles/r05_rdreq_c*.json). Lanes stay 2 KiB apart: a lane
 // scanning two strips (4 KiB apart, round-5 experiment) fetched less but ran the loop 17 %
 // slower (profiles/r05_ab14_*.log).
+// Measured (profiles/r05_ab20_*.log, r05_rdreq20_*_chain.json, r05_scan_stamps20_chain.log):
+// k_scan reads drop to 1.038x / 1.007x of its input, but it runs 4-7 % longer (configs[2] 3.77
+// against 3.60 ms): the block-1 step and the continuation run unpipelined (lookups, then the
+// chain), and the loop is not bound by HBM bytes alone. Off by default; the tests pass either way.
 #ifndef BSG_SCAN_CHAIN
 #define BSG_SCAN_CHAIN 0
 #endif
@@ -499,10 +503,15 @@ __device__ __forceinline__ uint32_t scan_span(const ScanArgs& a, const uint32_t*
                                               uint32_t (&w)[16], uint32_t& h,
                                               uint32_t (&hist)[64], uint64_t* t_warm) {
   const uint32_t nfull = j.len >> 6;
-  const uint32_t first = chained ? 1u : 0u;  // blocks folded in by the warm-up
-  const uint32_t nloop = nfull - first;      // (chained: nfull >= 1)
+  // chained: blocks 0 and 1 before the loop (the warm-up, then one block step), so that the
+  // loop's block pairs stay the two halves of one 128-byte line (a loop started at block 1 read
+  // every line half by half and k_scan read 1.22x its input, profiles/r05_rdreq19_*.json)
+  const uint32_t first = chained ? min(2u, nfull) : 0u;
+  const uint32_t nloop = nfull - first;
   const uint8_t* base = j.d + j.start + 64ull * first;
   load16(chained ? j.d + j.start : j.pre, w);
+  uint32_t w1b[16];  // chained: block 1 (the same line as block 0)
+  load16(chained ? j.d + j.start + 64ull * min(1u, nfull - 1) : j.pre, w1b);
   uint32_t w0[16], w1[16];
 #if BSG_SCAN_LOAD3
   // the strip's first line in flight with the warm-up block: one HBM round trip per strip start
@@ -529,8 +538,15 @@ __device__ __forceinline__ uint32_t scan_span(const ScanArgs& a, const uint32_t*
 #else
   (void)t_warm;
 #endif
-  // chained: block 0's last position, the one its window holds whole
+  // chained: block 0's last position (the one its window holds whole), then block 1
   uint32_t hits = (chained && (h & (WIDE ? 0xffffu : a.p.mask)) == 0) ? 1u : 0u;
+  if (chained && nfull >= 2) {
+    uint32_t hb[64];
+    lookup64(tab, w1b, hb, lane4);
+    hits |= chain64<WIDE, false>(tab, w1b, hist, hb, h, lane4, a.p.mask) ? 2u : 0u;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) hist[k] = hb[k];
+  }
   if (nloop)
     hits |= (uint32_t)scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0, 1>(a, tab, lane4, base, nloop,
                                                                      h, hist, w0, w1) << first;

@@ -6,6 +6,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 120 tools/ubench/lanes_align 2 0 > gpurun_out/r05_lanes_prio.log 2>&1 || exit $?
+timeout -k 10 120 tools/ubench/lanes_align 2 1 >> gpurun_out/r05_lanes_prio.log 2>&1 || exit $?
 BSG_LIB_PATH=bs_amd/variants/lib_chain.so timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05_pytest_gpu_call19.log 2>&1 || exit $?
 BSG_LIB_PATH=bs_amd/variants/lib_diagchain.so timeout -k 10 200 python tools/scan_stamps.py > gpurun_out/r05_scan_stamps19_chain.log 2>&1 || exit $?
 PMC="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"

@@ -57,7 +57,9 @@ __device__ __forceinline__ void lane_v4(uint32_t (&st)[8], uint32_t (&W)[16], co
 }
 
 template <int V>
-__global__ __launch_bounds__(512) void k_lanes(uint32_t* out, int blocks, uint64_t* stamps) {
+__global__ __launch_bounds__(512) void k_lanes(uint32_t* out, int blocks, uint64_t* stamps,
+                                               int prio = 0) {
+  if (prio && (threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(3);  // waves 0-3: one per SIMD
   extern __shared__ uint32_t pad[];
   if (blocks < 0) pad[threadIdx.x] = 0;  // never: keeps the LDS request (one workgroup per CU)
   uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
@@ -86,6 +88,7 @@ __global__ __launch_bounds__(512) void k_lanes(uint32_t* out, int blocks, uint64
 
 int main(int argc, char** argv) {
   const int wps = argc > 1 ? atoi(argv[1]) : 1;  // waves per SIMD
+  const int prio = argc > 2 ? atoi(argv[2]) : 0;  // 1: waves 0-3 of each workgroup at s_setprio 3
   const int cus = 256, blocks = 1000, tpb = 256 * wps, n = cus * tpb, nw = n / 64;
   uint32_t* o[5]; uint64_t* st;
   for (int v = 0; v < 5; ++v) (void)hipMalloc(&o[v], n * 32);
@@ -93,23 +96,29 @@ int main(int argc, char** argv) {
   uint64_t* hs = new uint64_t[nw];
   const char* names[5] = {"hipcc sha256_compress", "V1 aligned", "V2 +no copies", "V3 +K in SGPR",
                           "V4 +K in VGPRs"};
-  printf("%d wave(s) per SIMD\n", wps);
+  printf("%d wave(s) per SIMD%s\n", wps, prio ? ", waves 0-3 at s_setprio 3" : "");
   for (int r = 0; r < 3; ++r) {
     for (int v = 0; v < 5; ++v) {
       hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
       (void)hipEventRecord(e0);
       const size_t lds = 100 * 1024;
-      if (v == 0) hipLaunchKernelGGL(k_lanes<0>, dim3(cus), dim3(tpb), lds, 0, o[0], blocks, st);
-      if (v == 1) hipLaunchKernelGGL(k_lanes<1>, dim3(cus), dim3(tpb), lds, 0, o[1], blocks, st);
-      if (v == 2) hipLaunchKernelGGL(k_lanes<2>, dim3(cus), dim3(tpb), lds, 0, o[2], blocks, st);
-      if (v == 3) hipLaunchKernelGGL(k_lanes<3>, dim3(cus), dim3(tpb), lds, 0, o[3], blocks, st);
-      if (v == 4) hipLaunchKernelGGL(k_lanes<4>, dim3(cus), dim3(tpb), lds, 0, o[4], blocks, st);
+      if (v == 0) hipLaunchKernelGGL(k_lanes<0>, dim3(cus), dim3(tpb), lds, 0, o[0], blocks, st, prio);
+      if (v == 1) hipLaunchKernelGGL(k_lanes<1>, dim3(cus), dim3(tpb), lds, 0, o[1], blocks, st, prio);
+      if (v == 2) hipLaunchKernelGGL(k_lanes<2>, dim3(cus), dim3(tpb), lds, 0, o[2], blocks, st, prio);
+      if (v == 3) hipLaunchKernelGGL(k_lanes<3>, dim3(cus), dim3(tpb), lds, 0, o[3], blocks, st, prio);
+      if (v == 4) hipLaunchKernelGGL(k_lanes<4>, dim3(cus), dim3(tpb), lds, 0, o[4], blocks, st, prio);
       (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
       float ms; (void)hipEventElapsedTime(&ms, e0, e1);
       (void)hipMemcpy(hs, st, nw * 8, hipMemcpyDeviceToHost);
       double avg = 0; for (int i = 0; i < nw; ++i) avg += hs[i]; avg /= nw;
-      printf("%-22s %8.1f cycles/block/wave  %.3f ms  %.1f k blocks/us\n", names[v], avg / blocks,
+      double hi = 0, lo = 0; int nh = 0, nl = 0;  // waves 0-3 / 4-7 of each workgroup
+      for (int i = 0; i < nw; ++i) {
+        if ((i % (tpb / 64)) < 4) { hi += hs[i]; ++nh; } else { lo += hs[i]; ++nl; }
+      }
+      printf("%-22s %8.1f cycles/block/wave  %.3f ms  %.1f k blocks/us", names[v], avg / blocks,
              ms, (double)n * blocks / (ms * 1e3) / 1e3);
+      if (nl) printf("   waves 0-3 %.1f, 4-7 %.1f", hi / nh / blocks, lo / nl / blocks);
+      printf("\n");
     }
   }
   int bad = 0;
