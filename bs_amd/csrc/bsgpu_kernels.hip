@@ -1515,6 +1515,16 @@ __device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const
   }
 }
 
+// A region's pop counter holds two counts (round 5, BSG_LANE_YOUNG): the jobs taken from its
+// head (longest first, waves 0-3) in the low word, those taken from its tail (shortest first,
+// the young waves 4-7) in the high word; the jobs left are rorder[off + hd .. off + n - tl).
+// Returns hd, or n when no job is left.
+__device__ __forceinline__ uint64_t reg_head(const ShaArgs& a, uint32_t r, uint64_t n) {
+  const uint64_t v = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t hd = (uint32_t)v, tl = v >> 32;
+  return hd + tl < n ? hd : n;
+}
+
 // The region whose next job is the longest (longest-first across regions, so the last jobs
 // anywhere are short ones; ties: the first from `start` on), or R if every region is empty.
 // Called by a whole wave (some lanes may have left per-lane mode already); three dependent
@@ -1530,7 +1540,7 @@ __device__ uint32_t pick_region(const ShaArgs& a, uint32_t R, uint32_t start) {
   uint64_t key = 0;
   for (uint32_t r = rank; r < R; r += nact) {
     const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
-    const uint64_t h = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t h = reg_head(a, r, n);
     if (h < n) {
       const uint32_t len = (a.jinfo[a.rorder[o + h]] & ~kJobElig) + 1u;
       const uint64_t dist = (r + R - start) % R;
@@ -1570,7 +1580,7 @@ __device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
   bool has_mine = false;
   for (uint32_t r = rank; r < R; r += nact) {
     const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
-    const uint64_t h = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t h = reg_head(a, r, n);
     const uint32_t taken = n ? (uint32_t)(min(h, n) * (1ull << 20) / n) : (1u << 20);
     if (r == cur) {
       mine = taken;
@@ -1618,7 +1628,7 @@ __device__ uint32_t longer_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
   bool has_mine = false;
   for (uint32_t r = rank; r < R; r += nact) {
     const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
-    const uint64_t h = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t h = reg_head(a, r, n);
     uint32_t len = 0;
     if (h < n) len = (a.jinfo[a.rorder[o + h]] & ~kJobElig) + 1u;
     if (r == cur) {
@@ -1659,7 +1669,12 @@ __device__ uint32_t longer_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
 // one ended, and the whole wave waited for that atomic and ~4 dependent loads whenever any
 // lane switched. A job too short for the pipeline idles only its own lane until its successor
 // is ready; continued and open chunks (streaming) still take the synchronous sha_setup path.
-__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
+// young (BSG_LANE_YOUNG, waves 4-7 of a k_sha workgroup): the wave shares its SIMD with an older
+// one, which the SIMD serves first, so it runs at about half speed (tools/ubench/lanes_align.hip,
+// profiles/r05_lanes_prio.log: 11,300 against 5,700 cycles per block, the older wave unslowed).
+// It takes its region's jobs from the tail, shortest first, never a long one that would end
+// late, and does not chase other regions' longest jobs (no poll).
+__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) {
   constexpr int kBPI = BSG_LANE_BPI;  // blocks per iteration (per lane)
   const uint32_t lane = threadIdx.x & 63u;
   ShaJob jb;
@@ -1734,9 +1749,10 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
     } else if (stage == 1) {
       const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pop_base, pop_leader);
       const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pop_base >> 32), pop_leader);
-      const uint64_t local = (((uint64_t)hi << 32) | lo) + pop_rank;
-      q = pop_off + local;
-      dry = local >= pop_n;
+      // the counts before this pop: lo from the head, hi from the tail (reg_head)
+      const uint64_t local = (uint64_t)(young ? hi : lo) + pop_rank;
+      dry = local + (young ? lo : hi) >= pop_n;
+      q = young ? pop_off + pop_n - 1 - local : pop_off + local;
       stage = dry ? 0u : 2u;  // its job id is loaded below; else the region ran dry
     }
     if (__ballot(dry) && !all_done && pop_off == reg_off) {
@@ -1751,7 +1767,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
         reg_n = a.reg->off[reg + 1] - reg_off;
       }
     }
-    if (BSG_REGION_POLL && poll && !all_done && R > 1) {
+    if (BSG_REGION_POLL && poll && !all_done && R > 1 && !young) {
       // keep the regions level: move to the one furthest behind if this one is well ahead
       poll = false;
       const uint32_t r2 = BSG_REGION_BY_LEN ? longer_region(a, R, reg) : behind_region(a, R, reg);
@@ -1787,7 +1803,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
         uint32_t z;
         asm volatile("v_mov_b32 %0, 0" : "=v"(z));
         pop_base = atomicAdd(reinterpret_cast<unsigned long long*>(&a.reg->head[reg]) + z,
-                             (unsigned long long)__popcll(nm));
+                             (unsigned long long)__popcll(nm) << (young ? 32 : 0));
       }
       pop_leader = leader;
       pop_off = reg_off;
@@ -2637,6 +2653,22 @@ __device__ void sha_solo_fill(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t
 // drains the long-job queue in wave mode, then turns to per-lane mode (longest-first order).
 constexpr uint32_t kShaWaves = BSG_SHA_WAVES;
 static_assert(kShaWaves == 4 || kShaWaves == 8, "4 chain-capable waves per workgroup (+4 lane-only)");
+// BSG_LANE_YOUNG (round 5): four more waves per workgroup, one more per SIMD, in per-lane mode
+// only, taking each region's shortest jobs (sha_lane_mode's `young`). The SIMD serves the older
+// wave first, so waves 0-3 (chains, the longest per-lane jobs) keep their lone-wave speed and
+// the young ones fill the issue slots they leave (profiles/r05_lanes_prio.log: together 1.5x the
+// per-lane blocks of one wave). Round 2's eight-wave forms gave the longest per-lane jobs to
+// waves that shared a SIMD.
+// Measured (profiles/r05_ab21_*.log): configs[2] 886-902 against 914-970 GiB/s. The chains
+// slowed by ~4 % beside the young waves (long_end 12.27 against 11.80 ms), and the young waves'
+// last jobs, taken where the two ends of a region meet, were medium ones at half speed
+// (lane_end 13.8 against 12.6 ms); the per-lane work is mostly in the long jobs, so a young wave
+// held to short ones adds little. Off.
+#ifndef BSG_LANE_YOUNG
+#define BSG_LANE_YOUNG 0
+#endif
+static_assert(!BSG_LANE_YOUNG || kShaWaves == 4, "young waves join the four chain-capable ones");
+constexpr uint32_t kShaBlock = 64 * (kShaWaves + (BSG_LANE_YOUNG ? 4 : 0));
 
 // Two instantiations, launched back to back; the one that does not match the launch (helped
 // solo tickets or not, k_bucket_scan) returns at once. k_sha<false> holds no helper code, so
@@ -2644,7 +2676,7 @@ static_assert(kShaWaves == 4 || kShaWaves == 8, "4 chain-capable waves per workg
 // helper code in the same kernel made hipcc spill SGPRs inside that loop (configs[2] 880 ->
 // 760-840 GiB/s). k_sha<true> runs only lightly loaded launches, where per-lane mode is short.
 template <bool HELP>
-__global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
+__global__ __launch_bounds__(kShaBlock, 1) void k_sha(ShaArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (a.ctr->overflow || a.ctr->error) return;
   if ((a.ctr->helped != 0) != HELP) return;
@@ -2664,6 +2696,7 @@ __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
   // their speed, but the longest per-lane jobs, now sharing a SIMD, took 1.5x as long.
   const bool chain_wg = kShaWaves == 4 || (uint64_t)blockIdx.x * 4 < ntickets;
   if (kShaWaves > 4 && chain_wg && wv >= 4) return;
+  const bool young = BSG_LANE_YOUNG && wv >= 4;  // (takes part in the workgroup's barriers)
   uint32_t* ring = lds + (wv & 3u) * kRingWords;
   uint64_t t = ~0ull;
   bool helper_wg = false;
@@ -2679,7 +2712,7 @@ __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
       __syncthreads();
       const uint32_t c = wv & 1u;
       const uint64_t ht = hw * 2 + c;
-      if (ht < helped) {
+      if (ht < helped && !young) {
         __builtin_amdgcn_s_setprio(3);
         if (wv < 2) sha_solo_chain(a, M, ht, lds, c);
         else sha_solo_fill(a, M, ht, lds, c);
@@ -2687,7 +2720,7 @@ __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
       }
     }
   }
-  if (chain_wg && !helper_wg) {
+  if (chain_wg && !helper_wg && !young) {
     // row of ones after each wave's 64 K+W rows (the A lanes' kw in sha256_rounds_bank)
     for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 1u;
     // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
@@ -2705,7 +2738,7 @@ __global__ __launch_bounds__(64 * kShaWaves, 1) void k_sha(ShaArgs a) {
     }
     __builtin_amdgcn_s_setprio(0);
   }
-  sha_lane_mode(a, M);
+  sha_lane_mode(a, M, young);
   if ((threadIdx.x & 63u) == 0)
     atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->lane_end_rt),
               (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -3060,8 +3093,8 @@ static_assert(kHelpWords <= kHelpSlot && (kHelpSlot + 1) * 4 <= kShaLds,
 
 hipError_t launch_sha(const ShaArgs& a, uint64_t job_bound, hipStream_t s, int num_cus) {
   (void)job_bound;  // persistent: one workgroup per CU, waves loop over the job queues
-  hipLaunchKernelGGL(k_sha<true>, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
-  hipLaunchKernelGGL(k_sha<false>, dim3((uint32_t)num_cus), dim3(64 * kShaWaves), kShaLds, s, a);
+  hipLaunchKernelGGL(k_sha<true>, dim3((uint32_t)num_cus), dim3(kShaBlock), kShaLds, s, a);
+  hipLaunchKernelGGL(k_sha<false>, dim3((uint32_t)num_cus), dim3(kShaBlock), kShaLds, s, a);
   return hipGetLastError();
 }
 
