@@ -1443,10 +1443,10 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
 #endif                   // once per this many compressions
 
 #if BSG_LANE_DIAG
-// experiment: diag2[] = sums over waves of (0), lane-mode cycles, iterations, active
-// lane-iterations, waves (replaces the per-lane job timing)
+// experiment: diag2[] = sums over waves of cycles in the loop-top vmcnt(0) wait, lane-mode
+// cycles, iterations, active lane-iterations, waves (replaces the per-lane job timing)
 #define LANE_DIAG_INIT                                                                      \
-  uint64_t d_it = 0, d_act = 0, d_moves = 0;                                                 \
+  uint64_t d_it = 0, d_act = 0, d_moves = 0, d_wait = 0;                                     \
   const uint64_t d_t0 = __builtin_amdgcn_s_memtime();                                        \
   const uint64_t d_rt0 = __builtin_amdgcn_s_memrealtime();
 #define LANE_DIAG_ITER(active) \
@@ -1469,6 +1469,7 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
     }                                                                                        \
     if ((threadIdx.x & 63u) == 0) {                                                          \
       auto* d2 = reinterpret_cast<unsigned long long*>(a.ctr->diag2);                        \
+      atomicAdd(d2 + 0, (unsigned long long)d_wait);                                         \
       atomicAdd(d2 + 1, (unsigned long long)d_tot);                                          \
       atomicAdd(d2 + 2, (unsigned long long)m_it);                                           \
       atomicAdd(d2 + 3, (unsigned long long)m_act);                                          \
@@ -1731,7 +1732,13 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
     // Everything the last iteration issued (block prefetch, pipeline loads, the pop, the
     // record store) has had a whole compression to land: wait for all of it here, once, so
     // the compiler needs no wait further down.
+#if BSG_LANE_DIAG
+    const uint64_t d_w0 = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+    d_wait += __builtin_amdgcn_s_memtime() - d_w0;
+#else
+    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+#endif
     uint32_t W[kBPI][16];
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)  // garbage on idle lanes and past a job's end (never used)
