@@ -241,7 +241,7 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     best, nch, recs, reps = None, 0, [], []
     import gc
     gc.collect()
-    gc.disable()  # a cyclic-GC pass over the bench's heap inside a rep cost it ~4 ms (rep 2 of 3)
+    gc.disable()  # no cyclic-GC pass inside a timed rep (host-side noise, not the library's)
     for rep in range(4):  # rep 0 grows the pinned staging; best of the other three
         w.reset()
         recs = []
