@@ -1499,8 +1499,35 @@ __device__ __forceinline__ void pad_words_lane(int32_t valid, uint32_t (&W)[16])
 // The message words of block `blk` of the current job (rb holds it, prefetched). Idle lanes
 // (act false) skip the tail handling: their rb is a past-the-end block, and taking the tail
 // branch for them would run it for the whole wave in nearly every iteration.
+// BSG_LANE_UNI (round 5): per-lane mode's rare per-lane branches (a job's head or tail block, a
+// job's end, a job switch, the pipeline steps, the record store) sit behind a wave-uniform test
+// (a ballot), so the common iteration, where no lane takes them, runs no exec-mask bookkeeping
+// for them: the loop issued 46 SALU and 11 branches per block (profiles/r05_lane_mix.json).
+#ifndef BSG_LANE_UNI
+#define BSG_LANE_UNI 1
+#endif
+#define LANE_ANY(cond) (!BSG_LANE_UNI || __ballot(cond))
+
 __device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const RawBlock& rb,
                                            bool act, uint32_t (&W)[16]) {
+#if BSG_LANE_UNI
+  raw_to_words(rb, W);
+  const bool slow = 64ull * blk < jb.prefix;
+  const bool tail = act && rb.valid < 64;
+  if (__ballot(slow || tail)) {
+    if (slow) {
+      sha_load_slow(jb, blk, W);  // head block of a continued chunk (once per segment)
+    } else if (tail) {
+      pad_words_lane(rb.valid, W);
+      if (jb.fin && blk + 1 == jb.nblocks) {
+        const uint64_t bits = (jb.consumed + jb.L) * 8ull;
+        W[14] = (uint32_t)(bits >> 32);
+        W[15] = (uint32_t)bits;
+      }
+    }
+  }
+  return;
+#endif
   if (64ull * blk >= jb.prefix) {
     raw_to_words(rb, W);
     if (act && rb.valid < 64) {
@@ -1745,6 +1772,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
       lane_words(jb, blk + b, rb[b], act && blk + b < jb.nblocks, W[b]);
     // pipeline steps whose loads landed (the wait above): 5 -> 3, 2 -> 5, 1 -> 2 / 0
     bool dry = false;
+    if (LANE_ANY(stage == 5 || stage == 2 || stage == 1)) {
     if (stage == 5) {
       ld0 = ldn0;
       ld1 = ldn1;
@@ -1761,6 +1789,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
       dry = local + (young ? lo : hi) >= pop_n;
       q = young ? pop_off + pop_n - 1 - local : pop_off + local;
       stage = dry ? 0u : 2u;  // its job id is loaded below; else the region ran dry
+    }
     }
     if (__ballot(dry) && !all_done && pop_off == reg_off) {
       // the current region ran dry: move to the one with the most jobs left (wave-uniform,
@@ -1822,7 +1851,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
         stage = 1;
       }
     }
-    if (pend) {
+    if (LANE_ANY(pend) && pend) {
       ChunkRec* r = a.out + p_id;
       r->offset = p_start;
       r->len = p_len;
@@ -1858,7 +1887,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
 #endif
       }
     blk += kBPI;
-    if (act && blk >= jb.nblocks) {
+    if (LANE_ANY(act && blk >= jb.nblocks) && act && blk >= jb.nblocks) {
       act = false;
       if (jb.fin) {
         pend = true;
@@ -1881,7 +1910,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
         stamp = false;
       }
     }
-    if (!act) {
+    if (LANE_ANY(!act) && !act) {
       if (take) {  // its first block is on its way into rb
         jb.id = ld_id;
         jb.start = ld_start;
