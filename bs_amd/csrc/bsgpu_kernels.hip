@@ -1368,6 +1368,32 @@ __device__ __forceinline__ void raw_load(const uint8_t* dbase, uint64_t o0, uint
   rb.r[16] = al[16];
 }
 
+// N consecutive blocks from p (message offset o0 of a job of L message bytes): one aligned base
+// and one selector for all of them (p + 64 b keeps p's low two bits), the blocks at immediate
+// offsets of that base (BSG_LANE_LOADN, per-lane mode: the address and selector math ran once per
+// block; sel = the low two bits replicated into every byte by one v_perm, + 0x00010203).
+template <int N>
+__device__ __forceinline__ void raw_load_n(const uint8_t* p, uint64_t o0, uint64_t L,
+                                           RawBlock (&rb)[N]) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+  const uint32_t sh = (uint32_t)(addr & 3u);
+  const uint32_t sel = __builtin_amdgcn_perm(0u, sh, 0u) + 0x00010203u;
+  gu32* al = reinterpret_cast<gu32*>(addr & ~(uintptr_t)3);
+#pragma unroll
+  for (int b = 0; b < N; ++b) {
+    const int64_t vv = (int64_t)L - (int64_t)(o0 + 64ull * b);
+    rb[b].valid = vv < 0 ? -1 : (vv >= 64 ? 64 : (int32_t)vv);
+    rb[b].sel = sel;
+    gu32x4* q = reinterpret_cast<gu32x4*>(al + 16 * b);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u32x4 x = q[i];
+      rb[b].r[4 * i] = x.x; rb[b].r[4 * i + 1] = x.y; rb[b].r[4 * i + 2] = x.z; rb[b].r[4 * i + 3] = x.w;
+    }
+    rb[b].r[16] = al[16 * b + 16];
+  }
+}
+
 __device__ __forceinline__ void raw_to_words(const RawBlock& rb, uint32_t (&W)[16]) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(rb.r[i + 1], rb.r[i], rb.sel);
@@ -1870,11 +1896,23 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
     const uint64_t ld_start = ((uint64_t)ld0.w << 32) | ld0.z;
     const uint64_t ld_len = ((uint64_t)ld1.y << 32) | ld1.x;
     const bool take = !cont && ld_ready && !(ld1.w & kLaneJobSlow);
+#ifndef BSG_LANE_LOADN
+#define BSG_LANE_LOADN 1
+#endif
+#if BSG_LANE_LOADN
+    {
+      const uint64_t o0 = take ? 0ull : 64ull * (blk + kBPI);
+      const uint8_t* p0 = take ? reinterpret_cast<const uint8_t*>(ld_dptr)
+                               : jb.dbase + (o0 - jb.prefix);
+      raw_load_n<kBPI>(p0, o0, take ? ld_len : jb.L, rb);
+    }
+#else
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)
       raw_load(take ? reinterpret_cast<const uint8_t*>(ld_dptr) : jb.dbase,
                take ? 64ull * b : 64ull * (blk + kBPI + b), take ? 0u : jb.prefix,
                take ? ld_len : jb.L, rb[b]);
+#endif
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)
       if (act && blk + b < jb.nblocks) {
