@@ -15,4 +15,5 @@ PMC="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ
 timeout -s KILL 200 rocprofv3 --pmc $PMC -d gpurun_out/rdreq_final_c1 -o run --output-format csv -- python3 bench.py --cpu-sample-mib 0 --e2e-mib 0 --configs2-steps 0 --steps 1 --warmup 0 > gpurun_out/rdreq_final_c1.log 2>&1 || exit $?
 timeout -s KILL 200 rocprofv3 --pmc $PMC -d gpurun_out/rdreq_final_c2 -o run --output-format csv -- python3 bench.py --streams 256 --stream-mib 64 --cpu-sample-mib 0 --e2e-mib 0 --steps 1 --warmup 0 > gpurun_out/rdreq_final_c2.log 2>&1 || exit $?
 CTRS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_IFETCH GRBM_GUI_ACTIVE"
-timeout -s KILL 180 rocprofv3 --pmc $CTRS -d gpurun_out/pmc_final_c2 -o run --output-format csv -- python3 bench.py --streams 256 --stream-mib 64 --cpu-sample-mib 0 --e2e-mib 0 --steps 1 --warmup 1 > gpurun_out/pmc_final_c2.log 2>&1
+timeout -s KILL 180 rocprofv3 --pmc $CTRS -d gpurun_out/pmc_final_c2 -o run --output-format csv -- python3 bench.py --streams 256 --stream-mib 64 --cpu-sample-mib 0 --e2e-mib 0 --steps 1 --warmup 1 > gpurun_out/pmc_final_c2.log 2>&1 || exit $?
+BSG_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 2 --steps 5 --warmup 2 --cpu-sample-mib 0 --e2e-mib 0 --configs2-steps 0 > gpurun_out/r05_bench_n2_shared_gpu_rehearsal.log 2>&1
