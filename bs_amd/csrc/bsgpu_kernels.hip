@@ -33,9 +33,13 @@
 // against the solo chain's 1.19, so pair jobs above ~0.52 of the longest end after it; with
 // the faster per-lane mode (regions, round 2) per-lane jobs may reach 0.34 of it. Measured on
 // configs[2]: 50 / 34 with 16 solo tickets 888 GiB/s, 56 / 30 with 8 (the
-// earlier setting) 831 on the same box; configs[1] unchanged.
+// earlier setting) 831 on the same box; configs[1] unchanged. Round 5: with the octet chain at
+// 2,330 cycles per block (a group ticket ~3x the per-lane wave-cycles per block) and the pair
+// at about the per-lane cost, 53 / 56 / 58 gave 982-991 / 987-999 / 962-969 GiB/s and 50 gave
+// 977-978 (profiles/r05_ab29_c2.log, r05_ab30_c2.log): 55, a step below the 58 cliff where pair
+// jobs end after the longest chain.
 #ifndef BSG_TLEN_PCT
-#define BSG_TLEN_PCT 50
+#define BSG_TLEN_PCT 55
 #endif
 #ifndef BSG_PAIR_PCT
 #define BSG_PAIR_PCT 34
