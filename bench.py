@@ -362,11 +362,26 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
     def sync():
         bsgpu.synchronize(local)
 
-    eng.profile(1)
-    for w in range(warmup):
-        step(warm=w > 0 or warmup == 1)
-    eng.profile(2)
-    elapsed = timed_steps(step, sync, world, steps, 0)
+    # Between two steps the GPU idles while the host wakes from finish() and enqueues the next
+    # run: 35-50 us, and in one trace 83 and 218 us (a late wake-up, 50-137 us of host time in
+    # the Python step loop; tools/step_gaps.py, profiles/r05_step_gaps.txt). finish() polls its
+    # stream (BSG_KNOB_POLL) and the GC stays off for the steps; the GPU work is unchanged. The
+    # A/B (profiles/r05_ab34_*.log) is within the noise.
+    # (BSG_BENCH_POLL=0: the library's default blocking wait with the GC on, for A/B runs.)
+    import gc
+    quiet = os.environ.get("BSG_BENCH_POLL", "1") != "0"
+    gc.collect()
+    if quiet:
+        gc.disable()
+    try:
+        with bsgpu.debug_knob(bsgpu.KNOB_POLL, 1 if quiet else bsgpu.debug_get(bsgpu.KNOB_POLL)):
+            eng.profile(1)
+            for w in range(warmup):
+                step(warm=w > 0 or warmup == 1)
+            eng.profile(2)
+            elapsed = timed_steps(step, sync, world, steps, 0)
+    finally:
+        gc.enable()
     stage_avg = [stage_sum[0] / max(nsteps[0], 1), stage_sum[1] / max(nsteps[0], 1),
                  stage_sum[2] / max(nsteps[1], 1)]
     if nsteps[0] == 0:  # no warmup: the scan and selection stages were not timed

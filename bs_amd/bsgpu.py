@@ -183,7 +183,7 @@ def _p(a: np.ndarray, ct):
     return a.ctypes.data_as(ctypes.POINTER(ct))
 
 
-KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY = 1, 2, 3, 4  # bsg_debug_set knobs
+KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY, KNOB_POLL = 1, 2, 3, 4, 5  # bsg_debug_set
 
 
 def debug_get(knob: int) -> int:

@@ -264,13 +264,29 @@ std::atomic<int64_t>& knob(int k) {
     const char* e = std::getenv("BSG_EARLY");
     return e ? (int64_t)std::strtoull(e, nullptr, 10) : (int64_t)1;
   }()};
+  static std::atomic<int64_t> poll{[] {  // bsg_engine_finish: 1 polls the stream, 0 blocks
+    const char* e = std::getenv("BSG_POLL");
+    return e ? (int64_t)(std::strtoull(e, nullptr, 10) != 0) : (int64_t)0;
+  }()};
   static std::atomic<int64_t> none{0};
   switch (k) {
     case BSG_KNOB_SEQ_WAIT: return seq_wait;
     case BSG_KNOB_LONG_MODE: return long_mode;
     case BSG_KNOB_VERIFY_WINDOW: return verify_window;
     case BSG_KNOB_EARLY: return early;
+    case BSG_KNOB_POLL: return poll;
     default: return none;
+  }
+}
+// bsg_engine_finish's wait. hipStreamSynchronize sleeps on an interrupt once its short active
+// wait has passed and woke 7-43 us after the engine stream's last command ended (a configs[1]
+// step is ~9 ms; tools/step_gaps.py, profiles/r05_step_gaps.txt). BSG_KNOB_POLL queries the
+// stream in a loop instead: no wake-up latency, one host core busy for the run.
+hipError_t stream_wait(hipStream_t s) {
+  if (!knob(BSG_KNOB_POLL).load(std::memory_order_relaxed)) return hipStreamSynchronize(s);
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e != hipErrorNotReady) return e;
   }
 }
 uint32_t seq_wait_limit() { return (uint32_t)knob(BSG_KNOB_SEQ_WAIT).load(); }
@@ -642,7 +658,7 @@ struct bsg_engine {
     if (!enqueued) return BSG_ESTATE;
     for (int attempt = 0; attempt < 3; ++attempt) {
       HCHECK(hipMemcpyAsync(h_ctr.p, ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, stream));
-      HCHECK(hipStreamSynchronize(stream));
+      HCHECK(stream_wait(stream));
       last = *h_ctr.as<Counters>();
       if (!last.overflow) break;
       retry_cap = last.ncand + 1024;  // exact size for this input, then run again
@@ -1426,14 +1442,14 @@ struct bsg_ctx {
 extern "C" {
 
 int64_t bsg_debug_get(int k) {
-  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_EARLY) return -1;
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_POLL) return -1;
   return knob(k).load();
 }
 
 int bsg_debug_set(int k, int64_t value) {
-  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_EARLY || value < 0) return BSG_EINVAL;
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_POLL || value < 0) return BSG_EINVAL;
   if (k == BSG_KNOB_LONG_MODE && value > 2) return BSG_EINVAL;
-  if (k == BSG_KNOB_EARLY && value > 1) return BSG_EINVAL;
+  if ((k == BSG_KNOB_EARLY || k == BSG_KNOB_POLL) && value > 1) return BSG_EINVAL;
   if (k == BSG_KNOB_SEQ_WAIT && value > (int64_t)UINT32_MAX) return BSG_EINVAL;  // a u32 poll count
   knob(k).store(value);
   return BSG_OK;

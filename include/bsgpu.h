@@ -301,6 +301,9 @@ void bsg_reader_free(bsg_reader* r);
 #define BSG_KNOB_EARLY 4         /* BSG_EARLY: 1 (default) hashes the two longest chunks whose
                                   * ends are sure boundaries on a second stream from right after
                                   * candidate compaction (engine runs of >= 256 MiB); 0 off */
+#define BSG_KNOB_POLL 5          /* BSG_POLL: 1 makes bsg_engine_finish wait by polling its
+                                  * stream (one host core busy for the run, no interrupt wake-up
+                                  * latency); 0 (default) blocks in hipStreamSynchronize */
 int bsg_debug_set(int knob, int64_t value);
 int64_t bsg_debug_get(int knob); /* -1 for an unknown knob */
 

@@ -81,7 +81,7 @@ def test_debug_knobs_and_null_handles():
     from bs_amd import bsgpu
     L = bsgpu.lib()
     for knob in (bsgpu.KNOB_SEQ_WAIT, bsgpu.KNOB_LONG_MODE, bsgpu.KNOB_VERIFY_WINDOW,
-                 bsgpu.KNOB_EARLY):
+                 bsgpu.KNOB_EARLY, bsgpu.KNOB_POLL):
         old = bsgpu.debug_get(knob)
         assert old >= 0
         with bsgpu.debug_knob(knob, 1):
@@ -90,6 +90,7 @@ def test_debug_knobs_and_null_handles():
     assert L.bsg_debug_set(bsgpu.KNOB_LONG_MODE, 3) == -22   # 0 auto, 1 off, 2 all
     assert L.bsg_debug_set(bsgpu.KNOB_SEQ_WAIT, -1) == -22
     assert L.bsg_debug_set(bsgpu.KNOB_EARLY, 2) == -22       # 0 off, 1 on
+    assert L.bsg_debug_set(bsgpu.KNOB_POLL, 2) == -22        # 0 block, 1 poll
     assert L.bsg_debug_set(99, 0) == -22 and L.bsg_debug_get(99) == -1
     out = np.zeros(4, dtype=np.uint64)
     assert L.bsg_reader_stats(None, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == -22
