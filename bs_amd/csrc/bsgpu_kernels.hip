@@ -2738,7 +2738,9 @@ static_assert(kShaWaves == 4 || kShaWaves == 8, "4 chain-capable waves per workg
 // per-lane blocks of one wave). Round 2's eight-wave forms gave the longest per-lane jobs to
 // waves that shared a SIMD.
 // Measured (profiles/r05_ab21_*.log): configs[2] 886-902 against 914-970 GiB/s. The chains
-// slowed by ~4 % beside the young waves (long_end 12.27 against 11.80 ms), and the young waves'
+// slowed by ~4 % beside the young waves (long_end 12.27 against 11.80 ms) at the same cycles per
+// block (2,333-2,336 against 2,330-2,336): the clock fell, 2.23-2.24 against 2.32-2.34 GHz, so the
+// extra issue costs the chip power, not the chains' issue slots. And the young waves'
 // last jobs, taken where the two ends of a region meet, were medium ones at half speed
 // (lane_end 13.8 against 12.6 ms); the per-lane work is mostly in the long jobs, so a young wave
 // held to short ones adds little. Off.
