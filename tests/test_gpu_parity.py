@@ -291,6 +291,31 @@ def test_engine_device_resident_vs_oracle(gpu, oracle, table):
     eng.close()
 
 
+def test_engine_finish_polling(gpu, oracle, table):
+    """bsg_engine_finish with BSG_KNOB_POLL (the bench's wait: stream queries instead of a
+    blocking synchronize), over a run with early chains (>= 256 MiB) and repeated runs of one
+    engine: same records as the oracle, and the same as the blocking wait's."""
+    from bs_amd.synth import splitmix_array
+    lens = [300 << 20, 5_000_003]
+    got = {}
+    for poll in (1, 0, 1):
+        with gpu.debug_knob(gpu.KNOB_POLL, poll):
+            eng, buf, offs = _device_stream_run(gpu, lens, 0x5EED)
+            for _ in range(2):  # a second run of the same engine, waited the same way
+                eng.run(buf.ptr, offs, lens)
+                assert eng.finish() == len(eng.chunks())
+            got.setdefault(poll, []).append(as_tuples(eng.chunks()))
+            counts = eng.counts()
+            eng.close()
+            buf.free()
+    assert got[1][0] == got[0][0] == got[1][1]
+    k = 0
+    for i, n in enumerate(lens):
+        one = oracle.split(table, splitmix_array(0x5EED + i, n))
+        assert got[1][0][k:k + int(counts[i])] == as_tuples(one)
+        k += int(counts[i])
+
+
 @pytest.mark.slow
 def test_engine_1gib_full_parity(gpu, oracle, table):
     """BASELINE config 2 (1 GiB random stream, default params): full oracle comparison."""
