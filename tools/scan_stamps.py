@@ -46,6 +46,16 @@ def run(ns: int, mib: int, reps: int = 4) -> None:
         per = d[:6] / iters
         per[0] = d[0] / waves  # the prologue: once per wave
         acc.append((ms[0], per, d[5] / waves, d[8], clk, iters / waves))
+        if r == reps - 1:  # the workgroups' spans on the 100 MHz clock, from the first start
+            t0 = wg[:, 2].min()
+            st, en = (wg[:, 2] - t0) / 100.0, (wg[:, 3] - t0) / 100.0
+            q = [0, 10, 50, 90, 99, 100]
+            print(f"  last run, {len(wg)} workgroups: start us p{q} = "
+                  f"{np.round(np.percentile(st, q), 1).tolist()}, end us = "
+                  f"{np.round(np.percentile(en, q), 1).tolist()}")
+            late = np.argsort(en)[-6:]
+            print("  latest-ending workgroups (index, start, end us): " +
+                  ", ".join(f"({i}, {st[i]:.1f}, {en[i]:.1f})" for i in late))
     print(f"== {ns} x {mib} MiB: k_scan+k_refine stage {np.mean([a[0] for a in acc]):.3f} ms "
           f"(event-timed), workgroup clock {np.mean([a[4] for a in acc]):.3f} GHz, "
           f"{np.mean([a[5] for a in acc]):.1f} strips per wave")
