@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--e2e-mib", type=int, default=1024,
                     help="bytes of host-memory stream for the PCIe-inclusive streaming rate "
                          "(bsg_write -> records in host memory; 0: skip)")
+    ap.add_argument("--no-writer-e2e", dest="writer_e2e", action="store_false",
+                    help="skip the split.Writer -> store/mem leg (same host stream as --e2e-mib)")
     ap.add_argument("--configs2-steps", type=int, default=None,
                     help="timed steps of the nested configs[2] record (256 x 64 MiB on the same "
                          "GPU, N=1 default run only; default: --steps, 0: skip)")
@@ -224,11 +226,36 @@ def chain_roofline(diag: dict) -> dict | None:
             "frac_of_fetch_model": round(fetch / cyc, 4), "blocks": diag["long"].get("blocks")}
 
 
+def host_placement() -> dict:
+    """The process's CPU placement on the host: the CPUs it may run on and their NUMA nodes
+    (the GPU's node and the pinned stages' nodes come from bsg_stream_stats)."""
+    import glob
+    cpus = sorted(os.sched_getaffinity(0))
+    node_of = {}
+    for d in glob.glob("/sys/devices/system/node/node[0-9]*"):
+        try:
+            text = open(os.path.join(d, "cpulist")).read().strip()
+        except OSError:
+            continue
+        k = int(os.path.basename(d)[4:])
+        for part in filter(None, text.split(",")):
+            lo, _, hi = part.partition("-")
+            for c in range(int(lo), int(hi or lo) + 1):
+                node_of[c] = k
+    by_node = {}
+    for c in cpus:
+        by_node[node_of.get(c, -1)] = by_node.get(node_of.get(c, -1), 0) + 1
+    return {"cpus_allowed": len(cpus), "cpus_by_node": {str(k): v for k, v in sorted(by_node.items())},
+            "nodes": len(set(node_of.values())) or None}
+
+
 def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     """The streaming path from host memory: bsg_write of 32 MiB pieces (copy into a ring of
     pinned stages, each copied H2D into its 256 MiB device tile as it fills, three tiles in
     flight) -> split + SHA-256 -> records D2H -> bsg_drain. Best of 3 after one warm-up on the
-    same context (bsg_reset)."""
+    same context (bsg_reset). Every rep records where its time went (bsg_stream_stats: the host
+    copies into pinned staging, the H2D copies timed by HIP events on the copy stream, the NUMA
+    nodes of the GPU, the stages, the source and the copying threads)."""
     if mib <= 0:
         return None
     from bs_amd import bsgpu
@@ -238,25 +265,28 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     mv = memoryview(data)
     piece = 32 << 20
     w = bsgpu.StreamingSplitter(bits=bits, min_size=min_size, device=device)
-    best, nch, recs, reps = None, 0, [], []
+    best, nch, recs, reps, rep_stats = None, 0, [], [], []
     import gc
     gc.collect()
     gc.disable()  # no cyclic-GC pass inside a timed rep (host-side noise, not the library's)
-    for rep in range(4):  # rep 0 grows the pinned staging; best of the other three
-        w.reset()
-        recs = []
-        t0 = time.perf_counter()
-        for i in range(0, n, piece):
-            w.write(mv[i:i + piece])
+    try:
+        for rep in range(4):  # rep 0 grows the pinned staging; best of the other three
+            w.reset()
+            recs = []
+            t0 = time.perf_counter()
+            for i in range(0, n, piece):
+                w.write(mv[i:i + piece])
+                recs.append(w.drain())
+            tw = time.perf_counter() - t0
+            w.close()
             recs.append(w.drain())
-        tw = time.perf_counter() - t0
-        w.close()
-        recs.append(w.drain())
-        dt = time.perf_counter() - t0
-        reps.append([round(dt * 1e3, 2), round(tw * 1e3, 2)])
-        if rep and (best is None or dt < best):
-            best = dt
-    gc.enable()
+            dt = time.perf_counter() - t0
+            reps.append([round(dt * 1e3, 2), round(tw * 1e3, 2)])
+            rep_stats.append(w.stats())  # after the timed region
+            if rep and (best is None or dt < best):
+                best = dt
+    finally:
+        gc.enable()
     w.free()
     import numpy as np
     last = np.concatenate(recs)  # the last rep's records: checked against the oracle in main()
@@ -264,9 +294,58 @@ def end_to_end(mib: int, bits: int, min_size: int, device: int) -> dict | None:
     return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "chunks": nch,
             "records": last,
             "reps_ms": reps,  # [whole rep, of which the Write calls] per rep, rep 0 = warm-up
+            "reps_breakdown": rep_stats,
+            "host": host_placement(),
             "path": "host memory -> bsg_write (ring of 4 x 64 MiB pinned stages, each copied "
                     "H2D as it fills, on a copy stream into 4 device data slots) -> split + "
                     "SHA-256 on 3 engines -> records in host memory; tile 256 MiB"}
+
+
+def writer_e2e(mib: int, bits: int, min_size: int, device: int) -> dict | None:
+    """The drop-in surface itself (split/split.go:44-126 -> store/mem/mem.go:62-76): the C++
+    split::Writer -> MemStore over the same host-memory stream in 32 MiB Writes; every chunk Put
+    (aliasing the Write pieces, as store/mem keeps the caller's slice), the tree built with its
+    nodes hashed on the GPU and Put, Root computed. A fresh store per rep, the Writer's context
+    from the process pool (a server ingesting many files); rep 0 is the warm-up, best of the
+    other three. The Root is checked against the C oracle's split.Writer restatement after
+    timing (main())."""
+    if mib <= 0:
+        return None
+    from bs_amd import bsgpu
+    from bs_amd.synth import splitmix_array
+    n = mib << 20
+    data = splitmix_array(BASE_SEED, n)
+    mv = memoryview(data)
+    piece = 32 << 20
+    best, reps, roots, blobs = None, [], set(), 0
+    import gc
+    gc.collect()
+    gc.disable()
+    try:
+        for rep in range(4):
+            st = bsgpu.MemStore(device)
+            t0 = time.perf_counter()
+            w = bsgpu.Writer(st, bits=bits, min_size=min_size, fanout=8, device=device)
+            for i in range(0, n, piece):
+                w.write(mv[i:i + piece])
+            tw = time.perf_counter() - t0
+            w.close()
+            dt = time.perf_counter() - t0
+            roots.add(w.root)
+            tm = w.timings()
+            blobs = len(st)
+            w.free()
+            st.free()  # outside the timed region
+            reps.append({"ms": round(dt * 1e3, 2), "write_ms": round(tw * 1e3, 2), **tm})
+            if rep and (best is None or dt < best):
+                best = dt
+    finally:
+        gc.enable()
+    return {"value": round(n / best / 2**30, 3), "unit": "GiB/s", "bytes": n, "blobs": blobs,
+            "root": roots.pop().hex() if len(roots) == 1 else None, "data": data,
+            "reps": reps,  # rep 0 = warm-up; times in ms (bsg_writer_timings)
+            "path": "host memory -> C++ split::Writer (32 MiB Writes) -> chunks Put into "
+                    "store/mem, tree nodes hashed on the GPU and Put, Root"}
 
 
 # rocprofv3 names of each stage's kernels (k_sha: two instantiations launched back to back, one of
@@ -363,23 +442,18 @@ def device_leg(ns: int, nbytes: int, bits: int, min_size: int, steps: int, warmu
         bsgpu.synchronize(local)
 
     # Between two steps the GPU idles while the host wakes from finish() and enqueues the next
-    # run: 35-50 us, and in one trace 83 and 218 us (a late wake-up, 50-137 us of host time in
-    # the Python step loop; tools/step_gaps.py, profiles/r05_step_gaps.txt). finish() polls its
-    # stream (BSG_KNOB_POLL) and the GC stays off for the steps; the GPU work is unchanged. The
-    # A/B (profiles/r05_ab34_*.log) is within the noise.
-    # (BSG_BENCH_POLL=0: the library's default blocking wait with the GC on, for A/B runs.)
+    # run (tools/step_gaps.py, profiles/r05_step_gaps.txt): finish() polls its stream by the
+    # library's default (BSG_KNOB_POLL), and the Python GC stays off for the steps (harness
+    # noise: a GC pass in the step loop, not library work).
     import gc
-    quiet = os.environ.get("BSG_BENCH_POLL", "1") != "0"
     gc.collect()
-    if quiet:
-        gc.disable()
+    gc.disable()
     try:
-        with bsgpu.debug_knob(bsgpu.KNOB_POLL, 1 if quiet else bsgpu.debug_get(bsgpu.KNOB_POLL)):
-            eng.profile(1)
-            for w in range(warmup):
-                step(warm=w > 0 or warmup == 1)
-            eng.profile(2)
-            elapsed = timed_steps(step, sync, world, steps, 0)
+        eng.profile(1)
+        for w in range(warmup):
+            step(warm=w > 0 or warmup == 1)
+        eng.profile(2)
+        elapsed = timed_steps(step, sync, world, steps, 0)
     finally:
         gc.enable()
     stage_avg = [stage_sum[0] / max(nsteps[0], 1), stage_sum[1] / max(nsteps[0], 1),
@@ -549,6 +623,8 @@ def main():
 
     build_once(world, local)
     assert bsgpu.device_count() > local, "bench.py needs a GPU (the HIP path is the product)"
+    if os.environ.get("BSG_BENCH_INIT") == "1":  # bsg_init up front, as a server does (A/B)
+        bsgpu.init(local)
     nbytes = args.stream_mib << 20
     ns = args.streams
     leg = device_leg(ns, nbytes, args.bits, args.min_size, args.steps, args.warmup, world, rank,
@@ -579,6 +655,15 @@ def main():
               "chain_roofline": chain_roofline(leg2["diag"])}
     e2e = end_to_end(args.e2e_mib, args.bits, args.min_size, local) \
         if (rank == 0 and world == 1) else None
+    wr = writer_e2e(args.e2e_mib, args.bits, args.min_size, local) \
+        if (rank == 0 and world == 1 and args.writer_e2e) else None
+    if wr is not None:  # Root against the C oracle's split.Writer restatement, after timing
+        from oracle import oracle as O  # checker only
+        data = wr.pop("data")
+        ref_root, _ = O.writer_root(O.buzhash32_table(1), data, bits=args.bits,
+                                    min_size=args.min_size, fanout=8)
+        del data
+        wr["root_check"] = wr["root"] == ref_root.hex()
     if e2e is not None:
         # the e2e stream is the same SplitMix64 stream as configs[1]'s (seed BASE_SEED): when the
         # device leg's oracle split covered that whole stream, the host-path records are checked
@@ -608,6 +693,7 @@ def main():
                                  "serial SHA-256 chain (HBM frac reported)"),
             "cpu_baseline": leg["cpu"],
             "end_to_end": e2e,
+            "writer_e2e": wr,
             "stage_ms": {n: round(v, 4) for n, v in zip(STAGES, stage_avg)},
             "stage_ms_src": STAGE_SRC,
             "chunks_per_step": leg["chunks"],

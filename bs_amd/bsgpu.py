@@ -37,6 +37,37 @@ class Params(ctypes.Structure):
                 ("fanout", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+class StreamStats(ctypes.Structure):
+    """bsg_stream_stats (include/bsgpu.h): where a stream's host-to-device time went."""
+    _fields_ = [("host_bytes", ctypes.c_uint64), ("host_copy_ns", ctypes.c_uint64),
+                ("stage_wait_ns", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64),
+                ("h2d_copies", ctypes.c_uint64), ("h2d_busy_ns", ctypes.c_uint64),
+                ("h2d_span_ns", ctypes.c_uint64), ("copy_bytes_node", ctypes.c_uint64 * 4),
+                ("last_tile_ns", ctypes.c_uint64), ("tail_ns", ctypes.c_uint64),
+                ("gpu_node", ctypes.c_int32), ("stage_nodes", ctypes.c_uint32),
+                ("src_nodes", ctypes.c_uint32), ("copy_nt", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        def gbs(b, ns):
+            return round(b / ns, 2) if ns else None  # bytes per ns = GB/s
+
+        def nodes(mask):
+            return [k for k in range(32) if mask >> k & 1]
+        return {"host_copy_ms": round(self.host_copy_ns / 1e6, 3),
+                "host_copy_gbs": gbs(self.host_bytes, self.host_copy_ns),
+                "stage_wait_ms": round(self.stage_wait_ns / 1e6, 3),
+                "h2d_busy_ms": round(self.h2d_busy_ns / 1e6, 3),
+                "h2d_busy_gbs": gbs(self.h2d_bytes, self.h2d_busy_ns),
+                "h2d_span_ms": round(self.h2d_span_ns / 1e6, 3),
+                "h2d_span_gbs": gbs(self.h2d_bytes, self.h2d_span_ns),
+                "h2d_copies": int(self.h2d_copies),
+                "last_tile_ms": round(self.last_tile_ns / 1e6, 3),
+                "tail_after_h2d_ms": round(self.tail_ns / 1e6, 3),
+                "copy_mib_by_node": [int(b) >> 20 for b in self.copy_bytes_node],
+                "gpu_node": int(self.gpu_node), "stage_nodes": nodes(self.stage_nodes),
+                "src_nodes": nodes(self.src_nodes), "copy_nt": int(self.copy_nt)}
+
+
 CHUNK_DTYPE = np.dtype(
     [("offset", "<u8"), ("len", "<u8"), ("level", "<u4"), ("stream", "<u4"), ("ref", "u1", (32,))]
 )
@@ -139,6 +170,8 @@ def lib() -> ctypes.CDLL:
         "bsg_writer_write": (ctypes.c_int, [vp, vp, ctypes.c_size_t]),
         "bsg_writer_close": (ctypes.c_int, [vp]),
         "bsg_writer_root": (ctypes.c_int, [vp, vp]),
+        "bsg_writer_timings": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
+        "bsg_stream_stats_get": (ctypes.c_int, [vp, ctypes.POINTER(StreamStats)]),
         "bsg_writer_free": (None, [vp]),
         "bsg_reader_new": (vp, [vp, vp, ctypes.POINTER(ctypes.c_int)]),
         "bsg_reader_open": (vp, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
@@ -183,7 +216,8 @@ def _p(a: np.ndarray, ct):
     return a.ctypes.data_as(ctypes.POINTER(ct))
 
 
-KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY, KNOB_POLL = 1, 2, 3, 4, 5  # bsg_debug_set
+# bsg_debug_set
+KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY, KNOB_POLL, KNOB_COPY_NT = range(1, 7)
 
 
 def debug_get(knob: int) -> int:
@@ -555,6 +589,12 @@ class StreamingSplitter:
             self.commit(k)
             total += k
 
+    def stats(self) -> dict:
+        """bsg_stream_stats_get: host copy / H2D times and NUMA placement since open / reset."""
+        st = StreamStats()
+        _check(lib().bsg_stream_stats_get(self.h, ctypes.byref(st)), "bsg_stream_stats_get")
+        return st.as_dict()
+
     def drain(self) -> np.ndarray:
         n = lib().bsg_pending(self.h)
         out = np.zeros(max(n, 1), dtype=CHUNK_DTYPE)
@@ -706,6 +746,16 @@ class Writer:
         out = ctypes.create_string_buffer(32)
         _check(lib().bsg_writer_root(self.h, out), "Root")
         return out.raw
+
+    def timings(self) -> dict:
+        """bsg_writer_timings, in ms: Write copies, background Put + tree, waits for it, node
+        hashes, Close, Close's wait for the device, node-hash calls."""
+        t = (ctypes.c_double * 7)()
+        _check(lib().bsg_writer_timings(self.h, t), "bsg_writer_timings")
+        keys = ("copy_ms", "put_tree_ms", "join_ms", "node_hash_ms", "close_ms", "close_dev_ms")
+        out = {k: round(t[i] * 1e3, 3) for i, k in enumerate(keys)}
+        out["node_hash_calls"] = int(t[6])
+        return out
 
     def free(self):
         if self.h:

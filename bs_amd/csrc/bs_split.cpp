@@ -666,25 +666,71 @@ Status Writer::Process(const std::vector<bsg_chunk>& recs) {
 // A piece buffer. Large ones are their own anonymous mapping with transparent huge pages
 // requested: they are written once, kept by the store, and a fresh 4 KiB-page heap buffer
 // costs a page fault per 4 KiB on its first write (the largest cost of a Write before).
-static std::shared_ptr<uint8_t> alloc_piece(size_t n) {
-  constexpr size_t kHuge = 2ull << 20;
-  if (n >= kHuge) {
-    const size_t len = (n + kHuge - 1) & ~(kHuge - 1);
-    void* m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (m != MAP_FAILED) {
-      (void)::madvise(m, len, MADV_HUGEPAGE);
-      return std::shared_ptr<uint8_t>(static_cast<uint8_t*>(m),
-                                      [len](uint8_t* q) { ::munmap(q, len); });
+// Released mappings are kept for the next Writer in a process-wide pool of at most
+// kPiecePoolMax bytes (a server whose stores release their blobs — store/file after write-behind,
+// a dropped store/mem — reuses them): a fresh mapping costs its page faults plus the kernel
+// zeroing every page before the Write's copy writes it again, a second pass over host memory
+// (round 6: the Writer's copies took 25-30 ms per GiB against 7-10 for the raw path's,
+// profiles/r06_c1_copy_ab.log).
+namespace {
+constexpr size_t kPieceHuge = 2ull << 20;
+constexpr size_t kPiecePoolMax = 1ull << 30;
+struct PiecePool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free;  // mapping length -> mapping
+  size_t bytes = 0;
+};
+PiecePool& piece_pool() {
+  static auto* p = new PiecePool();  // never destroyed: mappings live until exit
+  return *p;
+}
+void piece_release(void* m, size_t len) {
+  PiecePool& pp = piece_pool();
+  {
+    std::lock_guard<std::mutex> g(pp.mu);
+    if (pp.bytes + len <= kPiecePoolMax) {
+      pp.free.emplace(len, m);
+      pp.bytes += len;
+      return;
     }
+  }
+  ::munmap(m, len);
+}
+void* piece_take(size_t len) {
+  PiecePool& pp = piece_pool();
+  std::lock_guard<std::mutex> g(pp.mu);
+  auto it = pp.free.find(len);
+  if (it == pp.free.end()) return nullptr;
+  void* m = it->second;
+  pp.free.erase(it);
+  pp.bytes -= len;
+  return m;
+}
+}  // namespace
+
+static std::shared_ptr<uint8_t> alloc_piece(size_t n) {
+  if (n >= kPieceHuge) {
+    const size_t len = (n + kPieceHuge - 1) & ~(kPieceHuge - 1);
+    void* m = piece_take(len);
+    if (!m) {
+      m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (m == MAP_FAILED) m = nullptr;
+      if (m) (void)::madvise(m, len, MADV_HUGEPAGE);
+    }
+    if (m)
+      return std::shared_ptr<uint8_t>(static_cast<uint8_t*>(m),
+                                      [len](uint8_t* q) { piece_release(q, len); });
   }
   return std::shared_ptr<uint8_t>(new (std::nothrow) uint8_t[n ? n : 1],
                                   std::default_delete<uint8_t[]>());
 }
 
 // Copies p[0..n) into dst (the Writer's piece) and, through the zero-copy window, into the
-// context's pinned staging: one read of the caller's bytes feeds both copies (each thread
-// copies a 64 KiB slice into the piece, then from there, still in cache, into the window), on
-// the process-wide copy pool (host_pool.h: BSG_COPY_THREADS threads shared by all Writers).
+// context's pinned staging: one read of the caller's bytes feeds both copies, streamed into the
+// two destinations with non-temporal stores (bsg::copy_nt2; with BSG_KNOB_COPY_NT off, each
+// thread copies a 64 KiB slice into the piece, then from there, still in cache, into the
+// window), on the process-wide copy pool (host_pool.h: BSG_COPY_THREADS threads shared by all
+// Writers).
 Status Writer::Copy(const uint8_t* p, size_t n, uint8_t* dst) {
   size_t done = 0;
   while (done < n) {
@@ -695,7 +741,12 @@ Status Writer::Copy(const uint8_t* p, size_t n, uint8_t* dst) {
     const size_t k = std::min(cap, n - done);
     const uint8_t* src = p + done;
     uint8_t* d1 = dst + done;
+    const bool use_nt = bsg::copy_nt_enabled();
     auto work = [=](size_t lo, size_t hi) {
+      if (use_nt) {  // one read of the caller's bytes, streamed into the piece and the stage
+        bsg::copy_nt2(d1 + lo, win + lo, src + lo, hi - lo);
+        return;
+      }
       constexpr size_t kSlice = 64 << 10;
       for (size_t o = lo; o < hi; o += kSlice) {
         const size_t m = std::min(kSlice, hi - o);
@@ -769,11 +820,16 @@ Status Writer::Close() {  // split/split.go:104-126
   if (!js.ok()) return sticky_ = js;
   // the last tiles finish one by one: each one's chunks are Put (background thread) while the
   // next is still on the device
+  double td = now_s();
   int rc = bsg_close_begin(ctx_);
   for (size_t left = 1; rc == BSG_OK && left;) {
     rc = bsg_close_step(ctx_, &left);
+    tm_.close_dev += now_s() - td;
     if (rc) break;
+    const double tj = now_s();
     Status s = Join();
+    td = now_s();
+    tm_.join += td - tj;
     if (!s.ok()) return sticky_ = s;
     std::vector<bsg_chunk> recs;
     if (TakeRecords(&recs)) Submit(&recs);
@@ -1334,6 +1390,11 @@ int bsg_writer_set_stream_base(bsg_writer* w, uint64_t base) {
 int bsg_writer_root(const bsg_writer* w, uint8_t out[32]) {
   if (!w || !out) return BSG_EINVAL;
   std::memcpy(out, w->w->Root().data(), 32);
+  return BSG_OK;
+}
+int bsg_writer_timings(const bsg_writer* w, double out[7]) {
+  if (!w || !out) return BSG_EINVAL;
+  w->w->Timings(out);
   return BSG_OK;
 }
 void bsg_writer_free(bsg_writer* w) { delete w; }

@@ -2,7 +2,7 @@
 // declared in include/bsgpu.h.
 //
 // A run = one launch sequence over a batch of stream segments (bsgpu_internal.h):
-//   k_start (descriptors in, counters zeroed) → k_scan → k_refine → prefix(strip counts) →
+//   k_start (descriptors in, counters zeroed) → k_scan (+ its exact pass) → prefix(strip counts) →
 //   k_compact → k_select → prefix(flags) → k_chunks → … → k_sha (→ k_early_fix), with the early
 //   chains (k_pick → k_early) on a second stream from k_compact on
 // Everything after k_scan sizes itself from device-side counters, so a run never waits on the
@@ -15,8 +15,11 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -266,7 +269,11 @@ std::atomic<int64_t>& knob(int k) {
   }()};
   static std::atomic<int64_t> poll{[] {  // bsg_engine_finish: 1 polls the stream, 0 blocks
     const char* e = std::getenv("BSG_POLL");
-    return e ? (int64_t)(std::strtoull(e, nullptr, 10) != 0) : (int64_t)0;
+    return e ? (int64_t)(std::strtoull(e, nullptr, 10) != 0) : (int64_t)1;
+  }()};
+  static std::atomic<int64_t> copy_nt{[] {  // Write copies: 1 non-temporal stores, 0 memcpy
+    const char* e = std::getenv("BSG_COPY_NT");
+    return e ? (int64_t)(std::strtoull(e, nullptr, 10) != 0) : (int64_t)1;
   }()};
   static std::atomic<int64_t> none{0};
   switch (k) {
@@ -275,18 +282,27 @@ std::atomic<int64_t>& knob(int k) {
     case BSG_KNOB_VERIFY_WINDOW: return verify_window;
     case BSG_KNOB_EARLY: return early;
     case BSG_KNOB_POLL: return poll;
+    case BSG_KNOB_COPY_NT: return copy_nt;
     default: return none;
   }
 }
 // bsg_engine_finish's wait. hipStreamSynchronize sleeps on an interrupt once its short active
 // wait has passed and woke 7-43 us after the engine stream's last command ended (a configs[1]
-// step is ~9 ms; tools/step_gaps.py, profiles/r05_step_gaps.txt). BSG_KNOB_POLL queries the
-// stream in a loop instead: no wake-up latency, one host core busy for the run.
+// step is ~9 ms; tools/step_gaps.py, profiles/r05_step_gaps.txt). BSG_KNOB_POLL (default on)
+// queries the stream instead, with a CPU pause between queries, for at most kPollMaxNs (a run
+// longer than that pays the wake-up once, relatively nothing) and then blocks: no wake-up latency
+// on a step-sized run, and no core spinning without bound.
+constexpr int64_t kPollMaxNs = 100'000'000;
 hipError_t stream_wait(hipStream_t s) {
   if (!knob(BSG_KNOB_POLL).load(std::memory_order_relaxed)) return hipStreamSynchronize(s);
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipStreamQuery(s);
     if (e != hipErrorNotReady) return e;
+    (void)hipGetLastError();
+    for (int i = 0; i < 32; ++i) _mm_pause();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::nanoseconds(kPollMaxNs))
+      return hipStreamSynchronize(s);
   }
 }
 uint32_t seq_wait_limit() { return (uint32_t)knob(BSG_KNOB_SEQ_WAIT).load(); }
@@ -497,14 +513,9 @@ struct bsg_engine {
     sa.lists = lists;
     sa.list_cap = list_cap;
     sa.list_cnt = reinterpret_cast<uint32_t*>(refine.as<uint64_t>() + lists * list_cap + 1);
-    sa.dbg = nullptr;
-#ifdef BSG_SCAN_DIAG  // experiment builds: k_scan's phase stamps into the Regions debug words
-    sa.dbg = reinterpret_cast<uint64_t*>(regions.as<uint8_t>() + offsetof(Regions, wdbg));
-    HCHECK(hipMemsetAsync(sa.dbg, 0, sizeof(Regions::wdbg), stream));
-#endif
     mark(0);
+    // k_scan: the fast pass, then each workgroup's exact pass over its own refine list
     if (strips) HCHECK(dbg("launch_scan", stream, launch_scan(sa, stream, num_cus)));
-    if (strips) HCHECK(dbg("launch_refine", stream, launch_refine(sa, stream, num_cus)));
     mark(1);
 
     PrefixArgs pa{};
@@ -802,6 +813,70 @@ void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
   copy_pool()->Run(n, fn);
 }
 
+bool copy_nt_enabled() { return knob(BSG_KNOB_COPY_NT).load(std::memory_order_relaxed) != 0; }
+
+namespace {
+// 64 bytes (one cache line) per iteration: four unaligned 16-byte loads, four streaming stores
+// to a 16-byte aligned destination (SSE2, every x86-64 host)
+inline void nt_lines(uint8_t* d, const uint8_t* s, size_t lines) {
+  for (size_t i = 0; i < lines; ++i, d += 64, s += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(d + 48), e);
+  }
+}
+// the same into two destinations; d2 streams only if it has d1's alignment mod 16, else it
+// takes ordinary stores
+inline void nt_lines2(uint8_t* d1, uint8_t* d2, const uint8_t* s, size_t lines, bool d2nt) {
+  for (size_t i = 0; i < lines; ++i, d1 += 64, d2 += 64, s += 64) {
+    __m128i v[4];
+    for (int j = 0; j < 4; ++j) v[j] = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + 16 * j));
+    for (int j = 0; j < 4; ++j) _mm_stream_si128(reinterpret_cast<__m128i*>(d1 + 16 * j), v[j]);
+    if (d2nt) {
+      for (int j = 0; j < 4; ++j) _mm_stream_si128(reinterpret_cast<__m128i*>(d2 + 16 * j), v[j]);
+    } else {
+      for (int j = 0; j < 4; ++j) _mm_storeu_si128(reinterpret_cast<__m128i*>(d2 + 16 * j), v[j]);
+    }
+  }
+}
+}  // namespace
+
+// The streaming stores are weakly ordered: each copy ends with an sfence, so the bytes are in
+// memory before the caller publishes them (a parallel_for's completion, then an H2D copy).
+void copy_nt(uint8_t* dst, const uint8_t* src, size_t n) {
+  const size_t head = std::min(n, (size_t)(-(uintptr_t)dst & 63));
+  std::memcpy(dst, src, head);
+  const size_t lines = (n - head) / 64;
+  nt_lines(dst + head, src + head, lines);
+  const size_t done = head + lines * 64;
+  std::memcpy(dst + done, src + done, n - done);
+  _mm_sfence();
+}
+
+void copy_nt2(uint8_t* d1, uint8_t* d2, const uint8_t* src, size_t n) {
+  const size_t head = std::min(n, (size_t)(-(uintptr_t)d1 & 63));
+  std::memcpy(d1, src, head);
+  std::memcpy(d2, src, head);
+  const size_t lines = (n - head) / 64;
+  const bool d2nt = (((uintptr_t)d1 ^ (uintptr_t)d2) & 15) == 0;
+  nt_lines2(d1 + head, d2 + head, src + head, lines, d2nt);
+  const size_t done = head + lines * 64;
+  std::memcpy(d1 + done, src + done, n - done);
+  std::memcpy(d2 + done, src + done, n - done);
+  _mm_sfence();
+}
+
+int cpu_node() {
+  unsigned cpu = 0, node = 0;
+  if (syscall(SYS_getcpu, &cpu, &node, nullptr) != 0) return -1;
+  return (int)node;
+}
+
 }  // namespace bsg
 
 constexpr int kMaxSlots = 8;
@@ -911,7 +986,47 @@ struct Stage {
   PinBuf buf;                // DMA staging (PinBuf::dma_only)
   hipEvent_t ev = nullptr;   // recorded after the H2D that reads the stage
   bool inflight = false;     // an H2D from it may still be running
+  hipEvent_t t0 = nullptr, t1 = nullptr;  // timing events around that H2D (bsg_stream_stats)
+  bool timed = false;        // t0/t1 recorded and not yet read
 };
+
+// NUMA node of the page holding p (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR; -1 unknown)
+int page_node(const void* p) {
+  int node = -1;
+  if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, 3UL) != 0) return -1;
+  return node;
+}
+
+// NUMA node of a HIP device, from its PCI function in sysfs (-1 unknown)
+int device_node(int device) {
+  static std::mutex mu;
+  static int cache[64];
+  static bool have[64];
+  std::lock_guard<std::mutex> g(mu);
+  const int k = device & 63;
+  if (have[k]) return cache[k];
+  char bus[64] = {0};
+  int node = -1;
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess) {
+    for (char* q = bus; *q; ++q) *q = (char)std::tolower((unsigned char)*q);
+    char path[160];
+    std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (FILE* f = std::fopen(path, "r")) {
+      if (std::fscanf(f, "%d", &node) != 1) node = -1;
+      std::fclose(f);
+    }
+  } else {
+    (void)hipGetLastError();
+  }
+  cache[k] = node;
+  have[k] = true;
+  return node;
+}
+
+uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now() - t0).count();
+}
 
 struct bsg_ctx {
   bsg_params params{};
@@ -941,6 +1056,14 @@ struct bsg_ctx {
   std::deque<bsg_chunk> ready;
   bool closed = false, started = false;
   int sticky = BSG_OK;
+  // bsg_stream_stats: counters since open / reset
+  bsg_stream_stats stats{};
+  std::atomic<uint64_t> node_bytes[4] = {};
+  hipEvent_t span0 = nullptr;  // recorded before the first H2D of the stream
+  bool span_set = false;
+  hipEvent_t tail0 = nullptr, tail1 = nullptr;  // the final tile's kernels: start, records out
+  bool tail_set = false;
+  int slast = -1;              // stage of the latest H2D
 
   size_t stage_size() const { return std::min(tile, kStageMax); }
 
@@ -950,7 +1073,12 @@ struct bsg_ctx {
     for (Stage& st : stages) {
       st.buf.dma_only = true;
       HCHECK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+      HCHECK(hipEventCreate(&st.t0));
+      HCHECK(hipEventCreate(&st.t1));
     }
+    HCHECK(hipEventCreate(&span0));
+    HCHECK(hipEventCreate(&tail0));
+    HCHECK(hipEventCreate(&tail1));
     std::memset(hist, 0, 64);
     std::memset(tail, 0, 64);
     return ensure_slot(0);  // the first tile's engine: errors surface at bsg_open
@@ -1006,9 +1134,63 @@ struct bsg_ctx {
     for (Stage& st : stages) {
       if (st.ev) (void)hipEventSynchronize(st.ev);
       StagePool::get().give(&st.buf);
-      if (st.ev) (void)hipEventDestroy(st.ev);
-      st.ev = nullptr;
+      for (hipEvent_t* e : {&st.ev, &st.t0, &st.t1}) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+      }
     }
+    for (hipEvent_t* e : {&span0, &tail0, &tail1}) {
+      if (*e) (void)hipEventDestroy(*e);
+      *e = nullptr;
+    }
+  }
+
+  // the finished H2D of stage st into the busy time
+  void harvest(Stage& st) {
+    if (!st.timed) return;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, st.t0, st.t1) == hipSuccess)
+      stats.h2d_busy_ns += (uint64_t)((double)ms * 1e6);
+    else
+      (void)hipGetLastError();
+    st.timed = false;
+  }
+
+  int get_stats(bsg_stream_stats* out) {
+    if (cstream) HCHECK(hipStreamSynchronize(cstream));
+    for (Stage& st : stages) harvest(st);
+    bsg_stream_stats s = stats;
+    if (span_set && slast >= 0) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, span0, stages[slast].t1) == hipSuccess)
+        s.h2d_span_ns = (uint64_t)((double)ms * 1e6);
+      else
+        (void)hipGetLastError();
+    }
+    if (tail_set) {
+      float ms = 0.f;
+      if (hipEventSynchronize(tail1) == hipSuccess &&
+          hipEventElapsedTime(&ms, tail0, tail1) == hipSuccess)
+        s.last_tile_ns = (uint64_t)((double)ms * 1e6);
+      else
+        (void)hipGetLastError();
+      if (slast >= 0 && hipEventElapsedTime(&ms, stages[slast].t1, tail1) == hipSuccess)
+        s.tail_ns = ms > 0.f ? (uint64_t)((double)ms * 1e6) : 0;
+      else
+        (void)hipGetLastError();
+    }
+    for (int k = 0; k < 4; ++k) s.copy_bytes_node[k] = node_bytes[k].load();
+    s.gpu_node = device_node(dev);
+    for (const Stage& st : stages) {
+      if (!st.buf.p) continue;
+      for (size_t at : {(size_t)0, st.buf.cap / 2}) {
+        const int nd = page_node(st.buf.as<uint8_t>() + at);
+        if (nd >= 0 && nd < 32) s.stage_nodes |= 1u << nd;
+      }
+    }
+    s.copy_nt = bsg::copy_nt_enabled() ? 1u : 0u;
+    *out = s;
+    return BSG_OK;
   }
 
   // Selection of slot i is done: learn its chunk count and where its open chunk starts. A
@@ -1049,6 +1231,10 @@ struct bsg_ctx {
       HCHECK(launch_copy_out(t.eng->out.p, rd, sizeof(bsg_chunk) * t.nchunks, t.eng->stream));
     HCHECK(launch_copy_out(t.eng->ctr.p, cd, sizeof(Counters), t.eng->stream));
     HCHECK(hipEventRecord(t.done_ev, t.eng->stream));
+    if (t.final_seg) {
+      HCHECK(hipEventRecord(tail1, t.eng->stream));
+      tail_set = true;
+    }
     t.recs_enq = true;
     return BSG_OK;
   }
@@ -1115,10 +1301,20 @@ struct bsg_ctx {
     if (rc) return rc;
     Stage& st = stages[scur];
     tail_append(st.buf.as<uint8_t>(), sfill);  // history for the next tile
+    if (!span_set) {
+      HCHECK(hipEventRecord(span0, cstream));
+      span_set = true;
+    }
+    HCHECK(hipEventRecord(st.t0, cstream));
     HCHECK(hipMemcpyAsync(data[dcur].dbuf.as<uint8_t>() + carry_cap + (fill - sfill), st.buf.p,
                           sfill, hipMemcpyHostToDevice, cstream));
+    HCHECK(hipEventRecord(st.t1, cstream));
     HCHECK(hipEventRecord(st.ev, cstream));
     st.inflight = true;
+    st.timed = true;
+    stats.h2d_bytes += sfill;
+    stats.h2d_copies++;
+    slast = scur;
     scur = (scur + 1) % kStages;
     sfill = 0;
     return BSG_OK;
@@ -1131,8 +1327,11 @@ struct bsg_ctx {
   int stage_ready(size_t need) {
     Stage& st = stages[scur];
     if (st.inflight) {
+      const auto t0 = std::chrono::steady_clock::now();
       HCHECK(hipEventSynchronize(st.ev));
+      stats.stage_wait_ns += ns_since(t0);
       st.inflight = false;
+      harvest(st);
     }
     const size_t full = stage_size();
     const bool big = pos - stream0 + fill >= full;  // past a stage's worth: whole stages
@@ -1173,6 +1372,7 @@ struct bsg_ctx {
     // the tile's kernels (and the carry copy into its data slot) run after its H2D copies
     HCHECK(hipEventRecord(t.copied_ev, cstream));
     HCHECK(hipStreamWaitEvent(e->stream, t.copied_ev, 0));
+    if (final_seg) HCHECK(hipEventRecord(tail0, e->stream));
     uint8_t* base = data[dcur].dbuf.as<uint8_t>();
     StreamDesc d{};
     d.data_off = carry_cap;
@@ -1252,6 +1452,10 @@ struct bsg_ctx {
   // has no length limit (split.Writer.Write has none, split/split.go:99-101): stream offsets are
   // u64 everywhere; only candidate positions inside one tile travel in 40-bit fields.
   int write(const uint8_t* p, size_t n) {
+    if (n >= (1u << 20)) {
+      const int nd = page_node(p);
+      if (nd >= 0 && nd < 32) stats.src_nodes |= 1u << nd;
+    }
     while (n) {
       if (fill == tile) {  // full tile and more data coming: submit it (never the last one)
         int rc = submit(false);
@@ -1260,7 +1464,10 @@ struct bsg_ctx {
       int rc = stage_ready(sfill + std::min(n, tile - fill));
       if (rc) return rc;
       const size_t k = std::min({n, tile - fill, stage_room()});
+      const auto t0 = std::chrono::steady_clock::now();
       par_copy(stages[scur].buf.as<uint8_t>() + sfill, p, k);
+      stats.host_copy_ns += ns_since(t0);
+      stats.host_bytes += k;
       sfill += k;
       fill += k;
       p += k;
@@ -1358,17 +1565,28 @@ struct bsg_ctx {
     return poll();
   }
 
-  static void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+  // Bytes into pinned staging on the copy pool; the bytes each thread copied are counted by the
+  // NUMA node it ran on (bsg_stream_stats)
+  void par_copy(uint8_t* dst, const uint8_t* src, size_t n) {
     constexpr size_t kPiece = 2ull << 20;  // per thread, at least
+    const bool nt_ok = bsg::copy_nt_enabled() && n >= kPiece;
+    auto one = [this, nt_ok](uint8_t* d, const uint8_t* s, size_t m) {
+      if (nt_ok)
+        bsg::copy_nt(d, s, m);
+      else
+        std::memcpy(d, s, m);
+      const int nd = bsg::cpu_node();
+      if (nd >= 0 && nd < 4) node_bytes[nd].fetch_add(m, std::memory_order_relaxed);
+    };
     const size_t nt = std::min<size_t>((size_t)copy_threads(), n / kPiece);
     if (nt <= 1) {
-      std::memcpy(dst, src, n);
+      one(dst, src, n);
       return;
     }
     const size_t per = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
     parallel_for((n + per - 1) / per, [=](size_t k) {
       const size_t o = k * per;
-      std::memcpy(dst + o, src + o, std::min(per, n - o));
+      one(dst + o, src + o, std::min(per, n - o));
     });
   }
 
@@ -1396,8 +1614,14 @@ struct bsg_ctx {
       Stage& st = stages[k];
       if (st.inflight) HCHECK(hipEventSynchronize(st.ev));
       st.inflight = false;
+      st.timed = false;
       StagePool::get().give(&st.buf);
     }
+    stats = bsg_stream_stats{};
+    for (auto& b : node_bytes) b.store(0);
+    span_set = false;
+    tail_set = false;
+    slast = -1;
     inflight.clear();
     ready.clear();
     cur = 0;
@@ -1442,14 +1666,15 @@ struct bsg_ctx {
 extern "C" {
 
 int64_t bsg_debug_get(int k) {
-  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_POLL) return -1;
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_LAST) return -1;
   return knob(k).load();
 }
 
 int bsg_debug_set(int k, int64_t value) {
-  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_POLL || value < 0) return BSG_EINVAL;
+  if (k < BSG_KNOB_SEQ_WAIT || k > BSG_KNOB_LAST || value < 0) return BSG_EINVAL;
   if (k == BSG_KNOB_LONG_MODE && value > 2) return BSG_EINVAL;
-  if ((k == BSG_KNOB_EARLY || k == BSG_KNOB_POLL) && value > 1) return BSG_EINVAL;
+  if ((k == BSG_KNOB_EARLY || k == BSG_KNOB_POLL || k == BSG_KNOB_COPY_NT) && value > 1)
+    return BSG_EINVAL;
   if (k == BSG_KNOB_SEQ_WAIT && value > (int64_t)UINT32_MAX) return BSG_EINVAL;  // a u32 poll count
   knob(k).store(value);
   return BSG_OK;
@@ -1752,8 +1977,8 @@ int bsg_engine_diag(const bsg_engine* e, uint64_t out[16]) {
   return BSG_OK;
 }
 
-// Experiment tooling (not in include/bsgpu.h): copies the region queues' state, including the
-// per-wave records of BSG_LANE_DIAG builds, after the last run.
+// Experiment tooling (not in include/bsgpu.h): copies the region queues' state after the last
+// run (tools/stress_regions.py).
 extern "C" int bsg_engine_regions_debug(bsg_engine* e, void* out, uint64_t nbytes) {
   if (!e || !out || !e->regions.p) return BSG_EINVAL;
   if (e->setdev()) return BSG_EDEVICE;
@@ -1946,6 +2171,12 @@ void bsg_free(bsg_ctx* c) {
   if (!c) return;
   c->release();
   delete c;
+}
+
+int bsg_stream_stats_get(bsg_ctx* c, bsg_stream_stats* out) {
+  if (!c || !out) return BSG_EINVAL;
+  if (hipSetDevice(c->dev) != hipSuccess) return BSG_EDEVICE;
+  return c->get_stats(out);
 }
 
 // bsg_split_hash_batch keeps a few engines (work buffers, pinned counters) for the next call:

@@ -146,9 +146,6 @@ struct Regions {
   uint64_t off[kMaxRegions + 1];             // region r's jobs: rorder[off[r] .. off[r + 1])
   uint64_t pad2_[7];
   uint32_t cnt[kRegionSegs * kMaxRegions];   // per segment and region: count, then offset
-  uint64_t wdbg[1024 * 8];                   // BSG_LANE_DIAG builds: per k_sha wave, per-lane
-                                             // mode entry / exit time, region moves, iterations,
-                                             // last wave-mode ticket, its start / end, blocks
 };
 
 // Early chains (round 4). A step is bound by its longest chunks' serial SHA-256 chains, and

@@ -20,12 +20,9 @@
 #include "bsgpu_launch.h"
 #include "sha256_device.h"
 
-// Wave-mode rounds: 1 (default) = skewed lane pairs, 9 VALU per round (sha256_rounds_skew,
-// 2,941 cycles per block on MI355X; the banked pair of sha256_rounds_bank takes 3,161); 0 = one
-// lane runs the whole round, 14 VALU (4,021 cycles). tools/ubench/skew.hip measures all three.
-#ifndef BSG_BANK_ROUNDS
-#define BSG_BANK_ROUNDS 1
-#endif
+// Wave-mode rounds run split over lanes: skewed pairs (9 VALU per round, 2,941 cycles per
+// block on MI355X) and skewed octets (8 VALU, 2,330 at round 5); one lane running the whole
+// round takes 14 VALU (4,021 cycles; tools/ubench/skew.hip, oct.hip).
 // Wave-mode tiers (k_bucket_scan), in percent of the longest job's blocks: jobs of at least
 // BSG_TLEN_PCT run on solo / group tickets (the kSolo longest one per wave, then 8 per wave),
 // jobs of BSG_PAIR_PCT up to that on pair tickets (32 per wave, one skewed lane pair each, ring
@@ -43,14 +40,6 @@
 #endif
 #ifndef BSG_PAIR_PCT
 #define BSG_PAIR_PCT 34
-#endif
-// Waves per k_sha workgroup (4; 8 is an experiment).
-#ifndef BSG_SHA_WAVES
-#define BSG_SHA_WAVES 4
-#endif
-// Solo tickets of lightly loaded launches run with a helper wave filling their rings (k_sha).
-#ifndef BSG_HELP_SOLO
-#define BSG_HELP_SOLO 1
 #endif
 // With the octet chains (round 2) a lightly loaded launch — all its blocks are less than a
 // tenth of what the chip's lanes hash while the longest chain runs — ends on the pair tickets
@@ -215,11 +204,7 @@ __device__ __forceinline__ uint32_t exact_block(const ScanArgs& a, const uint32_
 // folds to a constant.
 typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
 __device__ __forceinline__ uint32_t lds_at(const uint32_t*, uint32_t byte_addr) {
-#ifdef BSG_SCAN_NOLDS  // experiment builds only: no table lookups (results meaningless)
-  return byte_addr * 0x9E3779B1u;
-#else
   return *reinterpret_cast<lds_u32p>(static_cast<uintptr_t>(byte_addr));
-#endif
 }
 __device__ __forceinline__ bool table_at_lds0(const uint32_t* tab) {
   return (uint32_t)(uintptr_t)((lds_u32p)tab) == 0u;
@@ -273,38 +258,15 @@ __device__ __forceinline__ void lookup64(const uint32_t* tab, const uint32_t (&w
   for (int k = 0; k < 64; ++k) t[k] = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
 }
 
-// Fast-loop block loads. BSG_SCAN_NOLOAD (experiment builds only) replaces them with a cheap
-// register pattern to time the loop's compute alone; its results are meaningless.
-__device__ __forceinline__ void scan_load16(const uint8_t* p, uint32_t (&w)[16]) {
-#ifdef BSG_SCAN_NOLOAD
-  const uint32_t x = (uint32_t)(uintptr_t)p * 0x9E3779B1u;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) w[i] = x ^ (0x85EBCA6Bu * (uint32_t)(i + 1));
-#else
-  load16(p, w);
-#endif
-}
-
-template <int N>
-__device__ __forceinline__ void hit_mark(uint32_t (&hits)[N], uint32_t b, bool hit) {
-  if (N == 1) {
-    hits[0] |= hit ? 1u << b : 0u;
-  } else {
-#pragma unroll
-    for (int i = 0; i < N; ++i) hits[i] |= (hit && (b >> 5) == (uint32_t)i) ? 1u << (b & 31) : 0u;
-  }
-}
-
 // All full 64-byte blocks of a strip. On entry hA = table values of the 64 bytes before the
-// strip and h = the hash there. Blocks whose pre-filter hits are only marked here (one bit
-// each); k_refine scans them exactly afterwards, in block order, so the fast loop holds
+// strip, h = the hash there, and w0 / w1 = the strip's first line (blocks 0 and 1, loaded by
+// the caller beside the history block). Blocks whose pre-filter hits are only marked here (one
+// bit each); k_scan's exact pass scans them afterwards, in block order, so the fast loop holds
 // nothing but the two histories, two word blocks and the hash (no call, no scratch).
-constexpr int kHitWords = (kStrip / 64 + 31) / 32;
-static_assert(kHitWords == 1, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
+static_assert(kStrip / 64 <= 32, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
 
-// NH hit words: 1 for one strip (2: the round-5 two-strip span experiment).
-template <bool WIDE, bool PRE, int NH>
-__device__ __forceinline__ uint64_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
+template <bool WIDE>
+__device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
                                                      uint32_t lane4, const uint8_t* base,
                                                      uint32_t nfull, uint32_t& h,
                                                      uint32_t (&hA)[64], uint32_t (&w0)[16],
@@ -315,20 +277,16 @@ __device__ __forceinline__ uint64_t scan_full_blocks(const ScanArgs& a, const ui
   // the line is fetched once: loaded one block apart, the second half often found its line
   // evicted from L2 and fetched it again (k_scan read 1.5x its input on configs[1]).
   uint32_t n0[16], n1[16];
-  uint32_t hits[NH] = {};
-  if (!PRE) {  // (PRE: the caller loaded blocks 0 and 1 beside the history block)
-    scan_load16(base, w0);
-    scan_load16(base + 64ull * min(1u, nfull - 1), w1);  // (clamped, branch-free)
-  }
+  uint32_t hits = 0;
   lookup64(tab, w0, hB, lane4);                         // hB = block 0
   uint32_t b = 0;
   for (; b + 1 < nfull; b += 2) {
-    scan_load16(base + 64ull * min(b + 2, nfull - 1), n0);  // the next line
-    scan_load16(base + 64ull * min(b + 3, nfull - 1), n1);
+    load16(base + 64ull * min(b + 2, nfull - 1), n0);  // the next line (clamped, branch-free)
+    load16(base + 64ull * min(b + 3, nfull - 1), n1);
     // block b: out-going hA, in-coming hB; looks up block b+1 into hA
-    hit_mark(hits, b, chain64<WIDE, true>(tab, w1, hA, hB, h, lane4, mask));
+    hits |= chain64<WIDE, true>(tab, w1, hA, hB, h, lane4, mask) ? 1u << b : 0u;
     // block b+1: out-going hB, in-coming hA; looks up block b+2 into hB
-    hit_mark(hits, b + 1, chain64<WIDE, true>(tab, n0, hB, hA, h, lane4, mask));
+    hits |= chain64<WIDE, true>(tab, n0, hB, hA, h, lane4, mask) ? 1u << (b + 1) : 0u;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       w0[i] = n0[i];
@@ -336,12 +294,11 @@ __device__ __forceinline__ uint64_t scan_full_blocks(const ScanArgs& a, const ui
     }
   }
   if (b < nfull) {  // odd block count: the last block, then its values back into hA
-    hit_mark(hits, b, chain64<WIDE, false>(tab, w1, hA, hB, h, lane4, mask));
+    hits |= chain64<WIDE, false>(tab, w1, hA, hB, h, lane4, mask) ? 1u << b : 0u;
 #pragma unroll
     for (int k = 0; k < 64; ++k) hA[k] = hB[k];
   }
-  if constexpr (NH == 1) return hits[0];
-  else return ((uint64_t)hits[1] << 32) | hits[0];
+  return hits;
 }
 
 // strip0 (the streams' first strips) cached in LDS after the table, when it fits: the stream
@@ -410,219 +367,65 @@ __device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip,
   return j;
 }
 
-// Round 5: a strip's job from LDS alone. Each k_scan / k_refine workgroup caches, after strip0,
-// the two descriptor fields a strip needs (the segment's data offset; its length with the
-// finalize flag in bit 63), so the strip set-up runs no dependent global load: the round-4
-// StripJob read the descriptor from memory one strip ahead, but hipcc waited for that load
-// (vmcnt(0)) right where it was issued, a full HBM round trip at every strip start on every
-// wave of the CU.
-struct ScanStream {
-  uint64_t data_off;
-  uint64_t len_fin;   // len | finalize << 63
-};
-typedef const __attribute__((address_space(3))) ScanStream* lds_ssp;
-constexpr uint64_t kLenFin = 1ull << 63;
-
-#ifndef BSG_SCAN_SC
-#define BSG_SCAN_SC 1  // 0: strip jobs from the descriptors in global memory (round 4)
-#endif
-__device__ __forceinline__ lds_ssp cache_streams(uint32_t* lds_after, const ScanArgs& a) {
-  if (!BSG_SCAN_SC || a.nstreams + 1 > kStrip0Lds) return nullptr;
-  ScanStream* sc = reinterpret_cast<ScanStream*>(lds_after);
-  for (uint32_t i = threadIdx.x; i < a.nstreams; i += blockDim.x) {
-    const StreamDesc* sd = a.streams + i;
-    sc[i] = ScanStream{sd->data_off, sd->len | (sd->finalize ? kLenFin : 0ull)};
-  }
-  return (lds_ssp)(sc);
-}
-
-__device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip, lds_u64p s0,
-                                              lds_ssp sc) {
-  if (!sc) return strip_job(a, strip, s0);
-  const uint32_t s = find_stream(s0, a.nstreams, strip);
-  const uint64_t first = s0[s];
-  const uint64_t data_off = sc[s].data_off, len_fin = sc[s].len_fin;
-  const uint64_t seglen = len_fin & ~kLenFin;
-  StripJob j;
-  j.start = (strip - first) * (uint64_t)kStrip;
-  j.len = (uint32_t)min((uint64_t)kStrip, seglen - j.start);
-  j.d = a.data + data_off;
-  j.pre = j.start >= 64 ? j.d + j.start - 64 : a.streams[s].hist;  // an address, not a load
-  j.tail = (j.len & 63u) != 0 || (j.start + j.len == seglen && (len_fin & kLenFin) != 0);
-  j.fin = (len_fin & kLenFin) != 0;
-  j.seglen = seglen;
-  return j;
-}
-
-// The hash at a strip's first byte minus one from the table values t[] of the 64 bytes before
-// it: h = XOR_k rotl(t[k], 63 - k). Independent rotates folded by xor3 (the running form,
-// h = rotl1(h) ^ t[k], is a 128-instruction dependent chain).
-template <int R>
-__device__ __forceinline__ uint32_t rotl_c(uint32_t x) {
-  if constexpr ((R & 31) == 0) return x;
-  else return __builtin_amdgcn_alignbit(x, x, 32 - (R & 31));
-}
-template <int K = 0>
-__device__ __forceinline__ uint32_t fold64(const uint32_t (&t)[64]) {
-  if constexpr (K == 64) {
-    return 0u;
-  } else {
-    return xor3(rotl_c<63 - K>(t[K]), rotl_c<62 - K>(t[K + 1]), fold64<K + 2>(t));
-  }
-}
-
 // Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
-// hit bit per block whose pre-filter fires. Writes counts[strip] = 0 and returns whether
-// k_refine has exact work for the strip (hit blocks, the segment's < 64-byte tail, or the
-// final chunk's flush), with the hit mask in *hits_out.
-#ifndef BSG_SCAN_LOAD3
-#define BSG_SCAN_LOAD3 1  // the strip's first line loaded with its history block (0: round 4)
-#endif
-#ifndef BSG_SCAN_WARM
-#define BSG_SCAN_WARM 0  // 1: the history's lookups all issued, then folded by fold64 (round 5
-#endif                   // experiment); 0: the running form h = rotl1(h) ^ t
-// Fast pass over one strip: the rolling hash at every position of its full 64-byte blocks, a
-// hit bit per block whose pre-filter fires.
-//
-// BSG_SCAN_CHAIN (chained strips): lane l's strip follows lane l-1's in the same segment for
-// every lane but a wave's first and a segment's first strip. Such a strip does not read the 64
-// bytes before it: it warms up on its own block 0 (the hash at its byte 63, checked), and lane
-// l-1 checks positions 0..62 of it by running its hash on past its own end, with block 0's
-// words taken from lane l by a lane shift and its hit bit handed back the same way. The history
-// block was the second half of lane l-1's last line, read by the two lanes ~45 us apart, so
-// that line came from HBM twice: 128 of every 2,048 bytes (k_scan read 1.100x / 1.069x its
-// input on configs[1] / [2], profiles/r05_rdreq_c*.json). Lanes stay 2 KiB apart: a lane
-// scanning two strips (4 KiB apart, round-5 experiment) fetched less but ran the loop 17 %
-// slower (profiles/r05_ab14_*.log).
-// Measured (profiles/r05_ab20_*.log, r05_rdreq20_*_chain.json, r05_scan_stamps20_chain.log):
-// k_scan reads drop to 1.038x / 1.007x of its input, but it runs 4-7 % longer (configs[2] 3.77
-// against 3.60 ms): the block-1 step and the continuation run unpipelined (lookups, then the
-// chain), and the loop is not bound by HBM bytes alone. Off by default; the tests pass either way.
-#ifndef BSG_SCAN_CHAIN
-#define BSG_SCAN_CHAIN 0
-#endif
+// hit bit per block whose pre-filter fires. The strip's first line is loaded with its history
+// block (one HBM round trip per strip start instead of two; a short strip reads within
+// kReadSlack), then the window is warmed on the history in the running form h = rotl1(h) ^ t.
+// (Round 5 measured and dropped: the warm-up as independent rotates folded by xor3, and chained
+// strips — lane l continuing lane l-1's strip so that the history block is not read again —
+// which cut k_scan's reads from 1.069x to 1.007x of its input but ran 4-7 % longer,
+// profiles/r05_ab20_*.log: the loop is not bound by HBM bytes alone.)
 template <bool WIDE>
 __device__ __forceinline__ uint32_t scan_span(const ScanArgs& a, const uint32_t* tab,
-                                              uint32_t lane4, const StripJob& j, bool chained,
-                                              uint32_t (&w)[16], uint32_t& h,
-                                              uint32_t (&hist)[64], uint64_t* t_warm) {
+                                              uint32_t lane4, const StripJob& j, uint32_t& h,
+                                              uint32_t (&hist)[64]) {
   const uint32_t nfull = j.len >> 6;
-  // chained: blocks 0 and 1 before the loop (the warm-up, then one block step), so that the
-  // loop's block pairs stay the two halves of one 128-byte line (a loop started at block 1 read
-  // every line half by half and k_scan read 1.22x its input, profiles/r05_rdreq19_*.json)
-  const uint32_t first = chained ? min(2u, nfull) : 0u;
-  const uint32_t nloop = nfull - first;
-  const uint8_t* base = j.d + j.start + 64ull * first;
-  load16(chained ? j.d + j.start : j.pre, w);
-  uint32_t w1b[16];  // chained: block 1 (the same line as block 0)
-  load16(chained ? j.d + j.start + 64ull * min(1u, nfull - 1) : j.pre, w1b);
-  uint32_t w0[16], w1[16];
-#if BSG_SCAN_LOAD3
-  // the strip's first line in flight with the warm-up block: one HBM round trip per strip start
-  // instead of two (a short strip reads within kReadSlack)
-  scan_load16(base, w0);
-  scan_load16(base + 64ull * min(1u, nloop - 1), w1);
+  const uint8_t* base = j.d + j.start;
+  uint32_t w[16], w0[16], w1[16];
+  load16(j.pre, w);
+  load16(base, w0);
+  load16(base + 64ull * min(1u, nfull - 1), w1);
   __builtin_amdgcn_sched_barrier(0);
-#endif
   h = 0;
-#if BSG_SCAN_WARM
-#pragma unroll
-  for (int k = 0; k < 64; ++k) hist[k] = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
-  h = fold64(hist);
-#else
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
     uint32_t t = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
     h = rotl1(h) ^ t;
     hist[k] = t;
   }
-#endif
-#ifdef BSG_SCAN_DIAG
-  *t_warm = __builtin_amdgcn_s_memtime();
-#else
-  (void)t_warm;
-#endif
-  // chained: block 0's last position (the one its window holds whole), then block 1
-  uint32_t hits = (chained && (h & (WIDE ? 0xffffu : a.p.mask)) == 0) ? 1u : 0u;
-  if (chained && nfull >= 2) {
-    uint32_t hb[64];
-    lookup64(tab, w1b, hb, lane4);
-    hits |= chain64<WIDE, false>(tab, w1b, hist, hb, h, lane4, a.p.mask) ? 2u : 0u;
-#pragma unroll
-    for (int k = 0; k < 64; ++k) hist[k] = hb[k];
-  }
-  if (nloop)
-    hits |= (uint32_t)scan_full_blocks<WIDE, BSG_SCAN_LOAD3 != 0, 1>(a, tab, lane4, base, nloop,
-                                                                     h, hist, w0, w1) << first;
-  return hits;
+  return nfull ? scan_full_blocks<WIDE>(a, tab, lane4, base, nfull, h, hist, w0, w1) : 0u;
 }
 
-#ifndef BSG_SCAN_FUSE
-#define BSG_SCAN_FUSE 1  // k_scan workgroups refine their own lists (0: a k_refine dispatch)
-#endif
-#ifndef BSG_SCAN_WGLIST
-#define BSG_SCAN_WGLIST 1  // refine list per k_scan workgroup, appended through an LDS counter
-#endif                     // (0: one global list, appended by a returning global atomic per wave)
-
-// Appends the flagged strips of a wave to the refine list: entry = strip << 32 | hit mask.
-// BSG_SCAN_WGLIST: to the workgroup's own list (refine + blockIdx.x * list_cap), whose count is
-// an LDS word: a returning LDS atomic instead of a returning global one, whose vmcnt(0) wait
-// also drained the next strip's prefetched lines. The workgroup stores its count at exit.
+// Appends the flagged strips of a wave to its workgroup's refine list (refine + blockIdx.x *
+// list_cap): entry = strip << 32 | hit mask. The list's count is an LDS word, so the append is a
+// returning LDS atomic (a returning global one's vmcnt(0) wait also drained the next strip's
+// prefetched lines); the workgroup stores its count at exit.
 __device__ __forceinline__ void refine_append(const ScanArgs& a, bool flag, uint64_t strip,
                                               uint32_t hits, uint32_t* lds_cnt) {
   const uint64_t m = __ballot(flag);
   if (!m) return;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-#if BSG_SCAN_WGLIST
   uint32_t b = 0;
   if (lane == leader) b = atomicAdd(lds_cnt, (uint32_t)__builtin_popcountll(m));
   const uint64_t base = (uint64_t)blockIdx.x * a.list_cap + (uint32_t)__shfl((int)b, (int)leader);
-#else
-  (void)lds_cnt;
-  uint32_t base_lo = 0, base_hi = 0;
-  if (lane == leader) {
-    const uint64_t b = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->nrefine),
-                                 (unsigned long long)__builtin_popcountll(m));
-    base_lo = (uint32_t)b;
-    base_hi = (uint32_t)(b >> 32);
-  }
-  const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)base_hi, (int)leader) << 32) |
-                        (uint32_t)__shfl((int)base_lo, (int)leader);
-#endif
   if (flag) {
     const uint64_t below = m & ((1ull << lane) - 1ull);
     a.refine[base + (uint64_t)__builtin_popcountll(below)] = (strip << 32) | hits;
   }
 }
 
-// Calls f(entry) for this thread's share of the refine list(s). BSG_SCAN_WGLIST: workgroup g
-// of the consumer (k_refine, k_compact, k_rescan; their grids are ScanArgs::lists) walks k_scan
-// workgroup g's list, whose length is about the same for every list; else the grid strides
-// over the one global list.
+// Calls f(entry) for this thread's share of the refine lists: workgroup g of the consumer
+// (k_compact, k_rescan; their grids are ScanArgs::lists) walks k_scan workgroup g's list, whose
+// length is about the same for every list.
 template <class F>
 __device__ __forceinline__ void for_refine(const ScanArgs& a, uint32_t threads, F f) {
-#if BSG_SCAN_WGLIST
   for (uint32_t g = blockIdx.x; g < a.lists; g += gridDim.x) {
     const uint64_t n = a.list_cnt[g];
     const uint64_t* list = a.refine + (uint64_t)g * a.list_cap;
     for (uint64_t i = threadIdx.x; i < n; i += threads) f(list[i]);
   }
-#else
-  const uint64_t n = a.ctr->nrefine;
-  for (uint64_t i = (uint64_t)blockIdx.x * threads + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * threads)
-    f(a.refine[i]);
-#endif
 }
-
-// Per-wave s_memtime stamps of k_scan's phases (BSG_SCAN_DIAG experiment builds only): summed
-// over all waves into ScanArgs::dbg (tools/scan_stamps.py).
-#ifdef BSG_SCAN_DIAG
-#define SCAN_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define SCAN_STAMP(v)
-#endif
 
 // Exact candidates of one strip flagged by the fast pass, in position order: its hit blocks,
 // then the segment's tail (< 64 bytes), then Splitter.Close()'s flush of the final chunk (a
@@ -659,48 +462,33 @@ __device__ __forceinline__ uint32_t refine_strip(const ScanArgs& a, const uint32
   return c.count;
 }
 
-// k_scan's workgroup (BSG_SCAN_WGS threads, a strip each per iteration) and dynamic LDS: the
-// table (at address 0), strip0, the stream cache, the list count. A 256-thread workgroup (one
-// wave per SIMD) runs two per CU, so a CU's next workgroup starts when one ends instead of when
-// the CU's only one does (its slowest wave ends ~10 % after the average, profiles/r05_scan_stamps*);
-// two must fit the CU's 160 KiB: no stream cache, and strip0 two entries short for the count.
-#ifndef BSG_SCAN_WGS
-#define BSG_SCAN_WGS 256
-#endif
-// BSG_SCAN_DYN: the grid is what the chip holds at once (two workgroups per CU) and each
-// workgroup takes its next strip group from a ticket counter (Counters::scan_ticket) instead of
-// the fixed stride, so the workgroups of slow CUs take fewer groups and all end together. With
-// the fixed stride, 1,024 workgroups ran as two rounds of 512 and the step ended with the slowest
-// workgroup of the second round: wave life 1.61 ms on average, 2.05 at most, the kernel 3.6 ms
-// on configs[2] (profiles/r05_scan_stamps5_w256.log). A workgroup takes at most kScanDynShare
-// times its even share, which bounds its refine list.
-#ifndef BSG_SCAN_DYN
-#define BSG_SCAN_DYN 1
-#endif
+// k_scan's workgroup: 256 threads (one wave per SIMD), a strip each per iteration, two
+// workgroups per CU, so a CU's next workgroup starts when one ends instead of when the CU's only
+// one does (its slowest wave ends ~10 % after the average, profiles/r05_scan_stamps*); 512-thread
+// workgroups, one per CU, measured the same (profiles/r05_ab38_c1.log). Dynamic LDS: the table
+// (at address 0), strip0 (two entries short of kStrip0Lds, so that two workgroups fit the CU's
+// 160 KiB), the list count and two ticket slots.
+// The grid is what the chip holds at once (two workgroups per CU) and each workgroup takes its
+// next strip group from a ticket counter (Counters::scan_ticket) instead of a fixed stride, so
+// the workgroups of slow CUs take fewer groups and all end together. With the fixed stride,
+// 1,024 workgroups ran as two rounds of 512 and the step ended with the slowest workgroup of the
+// second round: wave life 1.61 ms on average, 2.05 at most, the kernel 3.6 ms on configs[2]
+// (profiles/r05_scan_stamps5_w256.log). A workgroup takes at most kScanDynShare times its even
+// share, which bounds its refine list.
 constexpr uint64_t kScanDynShare = 2;
-constexpr uint32_t kScanThreads = BSG_SCAN_WGS;
-static_assert(kScanThreads == 512 || kScanThreads == 256, "k_scan workgroup size");
-constexpr bool kScanPair = kScanThreads == 256;  // two workgroups per CU
-constexpr uint32_t kScanSpan = 1u;                         // strips per lane per iteration
-constexpr uint32_t kScanGroup = kScanThreads * kScanSpan;  // strips per workgroup iteration
-constexpr uint32_t kScanStrip0Cap = kScanPair ? kStrip0Lds - 2 : kStrip0Lds;
+constexpr uint32_t kScanThreads = 256;
+constexpr uint32_t kScanGroup = kScanThreads;  // strips per workgroup iteration
+constexpr uint32_t kScanStrip0Cap = kStrip0Lds - 2;
 constexpr uint32_t kScanLdsStrip0 = kTabRows * kTabRep * 4;
-constexpr uint32_t kScanLdsStreams = kScanLdsStrip0 + kScanStrip0Cap * 8;
-constexpr uint32_t kScanLdsCnt =
-    kScanLdsStreams + (kScanPair ? 0u : kStrip0Lds * (uint32_t)sizeof(ScanStream));
+constexpr uint32_t kScanLdsCnt = kScanLdsStrip0 + kScanStrip0Cap * 8;
 constexpr uint32_t kScanLds = kScanLdsCnt + 16u;  // the list count, 2 ticket slots
-static_assert(!kScanPair || 2 * kScanLds <= 160 * 1024, "two k_scan workgroups per CU");
+static_assert(2 * kScanLds <= 160 * 1024, "two k_scan workgroups per CU");
 
 // WIDE (split_bits >= 16, the packed 16-bit pre-filter) and the narrow form are separate
 // kernels, so each holds one copy of the fast loop and its registers.
-//
 template <bool WIDE>
 __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
-  SCAN_STAMP(d_t0);
-#ifdef BSG_SCAN_DIAG
-  const uint64_t d_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
   if (!table_at_lds0(tab)) {
     if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
     return;
@@ -709,18 +497,11 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   if (threadIdx.x == 0) *lds_cnt = 0u;
   load_table<kScanThreads>(tab, a.table);
   const lds_u64p s0 = cache_strip0(tab + kScanLdsStrip0 / 4, a, kScanStrip0Cap);
-  const lds_ssp sc = kScanPair ? nullptr : cache_streams(tab + kScanLdsStreams / 4, a);
   __syncthreads();
-  SCAN_STAMP(d_t1);
-#ifdef BSG_SCAN_DIAG
-  uint64_t d_job = 0, d_warm = 0, d_main = 0, d_app = 0, d_it = 0;
-#endif
   const uint32_t lane4 = (threadIdx.x & 63u) << 2;
   uint64_t g = blockIdx.x;
   StripJob job{};
-  if (g * kScanGroup + kScanSpan * threadIdx.x < a.nstrips)
-    job = strip_job(a, g * kScanGroup + kScanSpan * threadIdx.x, s0, sc);
-#if BSG_SCAN_DYN
+  if (g * kScanGroup + threadIdx.x < a.nstrips) job = strip_job(a, g * kScanGroup + threadIdx.x, s0);
   // group tickets: the first group is blockIdx.x, later ones gridDim.x + the counter's value.
   // Thread 0 takes the ticket after next while the current group is scanned; it reaches the
   // others through LDS slot (iteration & 1) behind the iteration's barrier (a slot is written
@@ -739,142 +520,46 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
   __syncthreads();
   gnext = tslot[0];
   taken += gnext < ngroups;
-  uint32_t it = 1;
-  for (; g < ngroups; ++it) {
-    SCAN_STAMP(t0);
-    const uint64_t strip = g * kScanGroup + kScanSpan * threadIdx.x;
+  for (uint32_t it = 1; g < ngroups; ++it) {
+    const uint64_t strip = g * kScanGroup + threadIdx.x;
     const StripJob cur = job;
-    const uint64_t next = gnext < ngroups ? gnext * kScanGroup + kScanSpan * threadIdx.x : ~0ull;
-    if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
+    const uint64_t next = gnext < ngroups ? gnext * kScanGroup + threadIdx.x : ~0ull;
+    if (next < a.nstrips) job = strip_job(a, next, s0);  // used one iteration later
     uint64_t tk = ~0ull;
     if (threadIdx.x == 0 && gnext < ngroups && taken < max_groups)
       tk = gridDim.x + atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->scan_ticket), 1ull);
-#else
-  for (; g * kScanGroup < a.nstrips; g += gridDim.x) {
-    SCAN_STAMP(t0);
-    const uint64_t strip = g * kScanGroup + kScanSpan * threadIdx.x;
-    const StripJob cur = job;
-    const uint64_t next = strip + (uint64_t)gridDim.x * kScanGroup;
-    if (next < a.nstrips) job = strip_job(a, next, s0, sc);  // used one iteration later
-#endif
-    SCAN_STAMP(t1);
-    uint64_t t2 = 0;  // (BSG_SCAN_DIAG: the end of the history's warm-up)
     bool flag = false;
     uint32_t hits = 0;
     const bool in = strip < a.nstrips;
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool chained = BSG_SCAN_CHAIN && in && lane != 0 && cur.start != 0 && cur.len >= 64;
-    uint32_t w[16], hist[64], h = 0;
-    if (in) hits = scan_span<WIDE>(a, tab, lane4, cur, chained, w, h, hist, &t2);
-#if BSG_SCAN_CHAIN
-    {
-      // positions 0..62 of lane l+1's strip, when it is chained to this one: its block 0 by a
-      // lane shift (every lane takes part), the check on the lanes whose successor is chained
-      const uint64_t cm = __ballot(chained);
-      const bool succ = lane < 63 && ((cm >> (lane + 1)) & 1ull);
-      uint32_t ws[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) ws[i] = (uint32_t)__shfl_down((int)w[i], 1);
-      bool hit_s = false;
-      if (succ) {  // (this strip is full: no tail, hist = its last block's table values)
-        uint32_t hn[64];
-        lookup64(tab, ws, hn, lane4);
-        uint32_t hh = h;
-        hit_s = chain64<WIDE, false>(tab, ws, hist, hn, hh, lane4, a.p.mask);
-      }
-      const bool from_pred = __shfl_up((int)hit_s, 1) != 0;
-      if (chained && from_pred) hits |= 1u;
-    }
-#endif
+    uint32_t hist[64], h = 0;
     if (in) {
+      hits = scan_span<WIDE>(a, tab, lane4, cur, h, hist);
       a.counts[strip] = 0u;
       flag = hits || cur.tail;
     }
-    SCAN_STAMP(t3);
     refine_append(a, flag, strip, hits, lds_cnt);
-#if BSG_SCAN_DYN
     if (threadIdx.x == 0) tslot[it & 1u] = (uint32_t)min(tk, (uint64_t)0xffffffffu);
     __syncthreads();
     g = gnext;
     gnext = g < ngroups ? tslot[it & 1u] : ~0ull;
     taken += gnext < ngroups;
-#endif
-    SCAN_STAMP(t4);
-#ifdef BSG_SCAN_DIAG
-    d_job += t1 - t0;
-    if (!t2) t2 = t3;  // (no strip for this wave's lane 0)
-    d_warm += t2 - t1;
-    d_main += t3 - t2;
-    d_app += t4 - t3;
-    d_it += 1;
-#endif
   }
-#if BSG_SCAN_WGLIST
   __syncthreads();
   const uint32_t nlist = *lds_cnt;
   if (threadIdx.x == 0) a.list_cnt[blockIdx.x] = nlist;
-#if BSG_SCAN_FUSE
-  // k_refine's exact pass over this workgroup's own list, here, with the table and strip0
-  // already in LDS: no dispatch, no table load, and a workgroup that ends early refines while
-  // the others still scan. (The list entries are this workgroup's own stores, ordered by the
-  // barrier above.)
-  {
-    const uint64_t* list = a.refine + (uint64_t)blockIdx.x * a.list_cap;
-    for (uint32_t i = threadIdx.x; i < nlist; i += kScanThreads) {
-      const uint64_t e = list[i];
-      const uint64_t strip = e >> 32;
-      const uint32_t n = refine_strip<false>(a, tab, lane4, strip, (uint32_t)e, 0, s0);
-      a.counts[strip] = n;
-      if (n > (uint32_t)kSlotCap)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
-    }
-  }
-#endif
-#endif
-#ifdef BSG_SCAN_DIAG
-  SCAN_STAMP(d_t2);
-  if (a.dbg && (threadIdx.x & 63u) == 0) {
-    unsigned long long* d = reinterpret_cast<unsigned long long*>(a.dbg);
-    atomicAdd(d + 0, (unsigned long long)(d_t1 - d_t0));  // prologue: table, strip0, streams
-    atomicAdd(d + 1, (unsigned long long)d_job);
-    atomicAdd(d + 2, (unsigned long long)d_warm);
-    atomicAdd(d + 3, (unsigned long long)d_main);
-    atomicAdd(d + 4, (unsigned long long)d_app);
-    atomicAdd(d + 5, (unsigned long long)(d_t2 - d_t0));  // the wave's whole life
-    atomicAdd(d + 6, (unsigned long long)d_it);
-    atomicAdd(d + 7, 1ull);                                // waves
-    atomicMax(d + 8, (unsigned long long)(d_t2 - d_t0));
-    if (threadIdx.x == 0 && blockIdx.x < 2000) {  // per workgroup: its span in cycles and in
-      d[16 + 4 * blockIdx.x] = d_t0;                  // 100 MHz realtime (the clock)
-      d[17 + 4 * blockIdx.x] = d_t2;
-      d[18 + 4 * blockIdx.x] = d_r0;
-      d[19 + 4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    }
-  }
-#endif
-}
-
-// Exact pass over the strips k_scan listed (a few percent of them on random data at the
-// default Bits 16; all of them on degenerate data), one per lane from the compacted list, so
-// the waves are full: exact counts into counts[], the first kSlotCap candidates into the
-// strip's slots; strips with more are left to k_rescan.
-// 4 waves per SIMD (<= 128 VGPRs): two workgroups per CU, as its LDS allows
-__global__ __launch_bounds__(kScanWG, 4) void k_refine(ScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t tab[];
-  if (!table_at_lds0(tab)) {
-    if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.ctr->error), 2ull);
-    return;
-  }
-  load_table(tab, a.table);
-  const lds_u64p s0 = cache_strip0(tab + kTabRows * kTabRep, a);
-  __syncthreads();
-  const uint32_t lane4 = (threadIdx.x & 63u) << 2;
-  for_refine(a, kScanWG, [&](uint64_t e) {
+  // The exact pass over this workgroup's own list, here, with the table and strip0 already in
+  // LDS: no dispatch, no table load, and a workgroup that ends early refines while the others
+  // still scan. (The list entries are this workgroup's own stores, ordered by the barrier
+  // above.)
+  const uint64_t* list = a.refine + (uint64_t)blockIdx.x * a.list_cap;
+  for (uint32_t i = threadIdx.x; i < nlist; i += kScanThreads) {
+    const uint64_t e = list[i];
     const uint64_t strip = e >> 32;
     const uint32_t n = refine_strip<false>(a, tab, lane4, strip, (uint32_t)e, 0, s0);
     a.counts[strip] = n;
-    if (n > (uint32_t)kSlotCap) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
-  });
+    if (n > (uint32_t)kSlotCap)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->rescan), 1ull);
+  }
 }
 
 // Slots -> the sorted candidate list, one lane per strip. No table and no re-scan registers,
@@ -929,7 +614,7 @@ __global__ __launch_bounds__(kScanWG, 2) void k_rescan(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Exclusive prefix sum u32 -> u64 (three phases). n is min(n_bound, *n_dev) when n_dev != null.
+// Exclusive prefix sum u32 -> u64 (k_prefix1). n is min(n_bound, *n_dev) when n_dev != null.
 // ---------------------------------------------------------------------------------------------
 constexpr int kScanT = 256, kScanItems = 8, kScanTile = kScanT * kScanItems;
 
@@ -939,102 +624,21 @@ __device__ __forceinline__ uint64_t scan_n(const PrefixArgs& a) {
   return n;
 }
 
-__global__ __launch_bounds__(kScanT) void k_prefix_reduce(PrefixArgs a) {
-  __shared__ uint64_t red[kScanT / 64];
-  if (a.skip_if && *a.skip_if) return;
-  const uint64_t n = scan_n(a);
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  if (base >= n) {
-    if (threadIdx.x == 0) a.partials[blockIdx.x] = 0;
-    return;
-  }
-  uint64_t s = 0;
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    const uint64_t idx = base + (uint64_t)i * kScanT + threadIdx.x;
-    if (idx < n) s += a.in[idx];
-  }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) a.partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
-__global__ __launch_bounds__(1024) void k_prefix_top(PrefixArgs a, uint64_t nblocks) {
-  __shared__ uint64_t wsum[16];
-  __shared__ uint64_t carry;
-  if (a.skip_if && *a.skip_if) return;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (uint64_t base = 0; base < nblocks; base += 1024) {
-    const uint64_t i = base + threadIdx.x;
-    const uint64_t v = i < nblocks ? a.partials[i] : 0;
-    uint64_t x = v;  // inclusive wave scan
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(x, o);
-      if ((threadIdx.x & 63) >= (uint32_t)o) x += y;
-    }
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
-    __syncthreads();
-    uint64_t pre = carry;
-    for (uint32_t wv = 0; wv < (threadIdx.x >> 6); ++wv) pre += wsum[wv];
-    if (i < nblocks) a.partials[i] = pre + x - v;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry = pre + x;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    *a.total = carry;
-    if (a.overflow && carry > a.cap) *a.overflow = 1;
-  }
-}
-
-__global__ __launch_bounds__(kScanT) void k_prefix_down(PrefixArgs a) {
-  __shared__ uint64_t wsum[kScanT / 64];
-  if (a.skip_if && *a.skip_if) return;
-  const uint64_t n = scan_n(a);
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
-  if (base >= n) return;
-  // thread t owns kScanItems consecutive elements
-  const uint64_t first = base + (uint64_t)threadIdx.x * kScanItems;
-  uint32_t v[kScanItems];
-  uint64_t s = 0;
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    v[i] = (first + i < n) ? a.in[first + i] : 0u;
-    s += v[i];
-  }
-  uint64_t x = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t y = __shfl_up(x, o);
-    if ((threadIdx.x & 63) >= (uint32_t)o) x += y;
-  }
-  if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = x;
-  __syncthreads();
-  uint64_t pre = a.partials[blockIdx.x];
-  for (uint32_t wv = 0; wv < (threadIdx.x >> 6); ++wv) pre += wsum[wv];
-  pre += x - s;
-  // Offsets are only read where the input is non-zero (k_compact / k_rescan for strips with
-  // candidates, k_chunks for flagged candidates), so only those are written: on configs[2]
-  // this is ~250 K of 8 M strip offsets.
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    if (first + i < n && v[i]) a.out[first + i] = pre;
-    pre += v[i];
-  }
-}
-
-// Single-pass exclusive prefix (round 5; decoupled look-back): one dispatch instead of
-// k_prefix_reduce -> k_prefix_top -> k_prefix_down, each of which cost a kernel boundary and a
-// pass over the input on the way to the early chains (configs[2]: 48 us for the strip counts).
-// Workgroup t takes tile t, publishes its tile's sum, and wave 0 looks back over the preceding
-// tiles 64 at a time, summing published tile sums until it meets a tile's published inclusive
-// prefix. Tiles go by blockIdx, not by a ticket counter: one counter hands out ≈ 88 tickets per
-// us (MI355X_MICROARCH.md, dequeue), 47 us for configs[2]'s 4,096 tiles, which made this kernel
-// slower than the three it replaces (profiles/r05_ab2.log). A workgroup waits only for tiles of
-// lower index, which the dispatcher has placed before it. A status word carries its value with its flag (the value in
-// the low 62 bits), so one relaxed agent-scope (sc1) store publishes it and one such load reads
-// it: no payload to fence. k_start zeroes the status words. A bounded poll flags a device error.
+// Single-pass exclusive prefix (round 5; decoupled look-back): one dispatch instead of a
+// reduce -> top -> down sequence of three, each of which cost a kernel boundary and a pass over
+// the input on the way to the early chains (configs[2]: 48 us for the strip counts). Workgroup t
+// takes tile t, publishes its tile's sum, and wave 0 looks back over the preceding tiles 64 at a
+// time, summing published tile sums until it meets a tile's published inclusive prefix. Tiles go
+// by blockIdx, not by a ticket counter: one counter hands out ≈ 88 tickets per us
+// (MI355X_MICROARCH.md, dequeue), 47 us for configs[2]'s 4,096 tiles, which made this kernel
+// slower than the three it replaced (profiles/r05_ab2.log). A status word carries its value with
+// its flag (the value in the low 62 bits), so one relaxed agent-scope (sc1) store publishes it and
+// one such load reads it: no payload to fence. k_start zeroes the status words.
+// Forward progress rests on in-order dispatch: the command processor hands out a grid's
+// workgroups in blockIdx order, each XCD's share in order too, so every tile a workgroup waits
+// for has been dispatched before it (it is resident or has finished) and a waiting workgroup never
+// holds back the one it waits for. Should that ever fail, the bounded poll (kPfxPolls sleeps,
+// ~1 s) ends the wait and flags device error 32 instead of hanging the GPU.
 constexpr uint64_t kPfxAgg = 1ull << 62, kPfxInc = 2ull << 62, kPfxVal = kPfxAgg - 1;
 constexpr uint32_t kPfxPolls = 1u << 22;
 
@@ -1045,13 +649,12 @@ __device__ __forceinline__ void pfx_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kScanT) void k_prefix1(PrefixArgs a, uint64_t ntiles) {
+__global__ __launch_bounds__(kScanT) void k_prefix1(PrefixArgs a) {
   __shared__ uint64_t wsum[kScanT / 64];
   __shared__ uint64_t sh_excl;
   if (a.skip_if && *a.skip_if) return;
   const uint64_t n = scan_n(a);
   uint64_t* status = a.partials;
-  (void)ntiles;
   const uint64_t t = blockIdx.x;
   const uint64_t base = t * (uint64_t)kScanTile;
   if (base >= n && t != 0) return;  // past the data: nobody looks back at this tile
@@ -1117,7 +720,9 @@ __global__ __launch_bounds__(kScanT) void k_prefix1(PrefixArgs a, uint64_t ntile
   }
   __syncthreads();
   pre += sh_excl;
-  // offsets only where the input is non-zero (the only offsets ever read, as k_prefix_down)
+  // Offsets are only read where the input is non-zero (k_compact / k_rescan for strips with
+  // candidates, k_chunks for flagged candidates), so only those are written: on configs[2]
+  // this is ~250 K of 8 M strip offsets.
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
     if (first + i < n && v[i]) a.out[first + i] = pre;
@@ -1374,8 +979,8 @@ __device__ __forceinline__ void raw_load(const uint8_t* dbase, uint64_t o0, uint
 
 // N consecutive blocks from p (message offset o0 of a job of L message bytes): one aligned base
 // and one selector for all of them (p + 64 b keeps p's low two bits), the blocks at immediate
-// offsets of that base (BSG_LANE_LOADN, per-lane mode: the address and selector math ran once per
-// block; sel = the low two bits replicated into every byte by one v_perm, + 0x00010203).
+// offsets of that base (per-lane mode, round 5: the address and selector math ran once per
+// block before; sel = the low two bits replicated into every byte by one v_perm, + 0x00010203).
 template <int N>
 __device__ __forceinline__ void raw_load_n(const uint8_t* p, uint64_t o0, uint64_t L,
                                            RawBlock (&rb)[N]) {
@@ -1458,59 +1063,12 @@ __device__ void sha_finish(const ShaArgs& a, const ShaJob& jb, const uint32_t (&
   }
 }
 
-#ifndef BSG_LANE_DIAG
-#define BSG_LANE_DIAG 0
-#endif
 #ifndef BSG_LANE_LEAD
 #define BSG_LANE_LEAD 4  // iterations before a job's end at which its successor is popped
 #endif
-#ifndef BSG_LANE_ASM
-#define BSG_LANE_ASM 2   // per-lane compressions as the aligned asm statement (sha256_device.h):
-#endif                   // 2 with K in 64 resident VGPRs, 1 with K through an SGPR; 0: hipcc's
-                         // schedule of sha256_compress (k_sha 13.44 vs 13.10 ms at 1, configs[2])
-#ifndef BSG_LANE_BPI
-#define BSG_LANE_BPI 2   // blocks per per-lane iteration: the job-switch and queue logic runs
-#endif                   // once per this many compressions
-
-#if BSG_LANE_DIAG
-// experiment: diag2[] = sums over waves of cycles in the loop-top vmcnt(0) wait, lane-mode
-// cycles, iterations, active lane-iterations, waves (replaces the per-lane job timing)
-#define LANE_DIAG_INIT                                                                      \
-  uint64_t d_it = 0, d_act = 0, d_moves = 0, d_wait = 0;                                     \
-  const uint64_t d_t0 = __builtin_amdgcn_s_memtime();                                        \
-  const uint64_t d_rt0 = __builtin_amdgcn_s_memrealtime();
-#define LANE_DIAG_ITER(active) \
-  d_it += 1;                   \
-  d_act += (uint64_t)__popcll(__ballot(active));
-#define LANE_DIAG_END                                                                       \
-  {                                                                                          \
-    const uint64_t d_tot = __builtin_amdgcn_s_memtime() - d_t0;                              \
-    const uint32_t wid = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);                \
-    if ((threadIdx.x & 63u) == 0 && wid < 1024) {                                            \
-      a.reg->wdbg[8 * wid + 0] = d_rt0;                                                      \
-      a.reg->wdbg[8 * wid + 1] = __builtin_amdgcn_s_memrealtime();                           \
-      a.reg->wdbg[8 * wid + 2] = d_moves;                                                    \
-      a.reg->wdbg[8 * wid + 3] = d_it;                                                       \
-    }                                                                                        \
-    uint64_t m_it = d_it, m_act = d_act;                                                     \
-    for (int o = 32; o > 0; o >>= 1) {                                                       \
-      m_it = max(m_it, (uint64_t)__shfl_xor((long long)m_it, o));                            \
-      m_act = max(m_act, (uint64_t)__shfl_xor((long long)m_act, o));                         \
-    }                                                                                        \
-    if ((threadIdx.x & 63u) == 0) {                                                          \
-      auto* d2 = reinterpret_cast<unsigned long long*>(a.ctr->diag2);                        \
-      atomicAdd(d2 + 0, (unsigned long long)d_wait);                                         \
-      atomicAdd(d2 + 1, (unsigned long long)d_tot);                                          \
-      atomicAdd(d2 + 2, (unsigned long long)m_it);                                           \
-      atomicAdd(d2 + 3, (unsigned long long)m_act);                                          \
-      atomicAdd(d2 + 4, 1ull);                                                               \
-    }                                                                                        \
-  }
-#else
-#define LANE_DIAG_INIT uint64_t d_moves = 0;
-#define LANE_DIAG_ITER(active)
-#define LANE_DIAG_END (void)d_moves;
-#endif
+// Blocks per per-lane iteration: the job-switch and queue logic runs once per this many
+// compressions (3 and 4 measured slower, round 5).
+constexpr int kLaneBPI = 2;
 
 // Tail block, cheaper form for the per-lane loop: words before the one holding byte `valid`
 // stay, that word keeps its valid bytes and gets the 0x80, later words are zero (valid -1: a
@@ -1529,18 +1087,14 @@ __device__ __forceinline__ void pad_words_lane(int32_t valid, uint32_t (&W)[16])
 // The message words of block `blk` of the current job (rb holds it, prefetched). Idle lanes
 // (act false) skip the tail handling: their rb is a past-the-end block, and taking the tail
 // branch for them would run it for the whole wave in nearly every iteration.
-// BSG_LANE_UNI (round 5): per-lane mode's rare per-lane branches (a job's head or tail block, a
-// job's end, a job switch, the pipeline steps, the record store) sit behind a wave-uniform test
-// (a ballot), so the common iteration, where no lane takes them, runs no exec-mask bookkeeping
-// for them: the loop issued 46 SALU and 11 branches per block (profiles/r05_lane_mix.json).
-#ifndef BSG_LANE_UNI
-#define BSG_LANE_UNI 1
-#endif
-#define LANE_ANY(cond) (!BSG_LANE_UNI || __ballot(cond))
+// Per-lane mode's rare per-lane branches (a job's head or tail block, a job's end, a job switch,
+// the pipeline steps, the record store) sit behind a wave-uniform test (a ballot), so the common
+// iteration, where no lane takes them, runs no exec-mask bookkeeping for them: without it the
+// loop issued 46 SALU and 11 branches per block (round 5, profiles/r05_lane_mix.json).
+#define LANE_ANY(cond) (__ballot(cond))
 
 __device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const RawBlock& rb,
                                            bool act, uint32_t (&W)[16]) {
-#if BSG_LANE_UNI
   raw_to_words(rb, W);
   const bool slow = 64ull * blk < jb.prefix;
   const bool tail = act && rb.valid < 64;
@@ -1556,31 +1110,14 @@ __device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const
       }
     }
   }
-  return;
-#endif
-  if (64ull * blk >= jb.prefix) {
-    raw_to_words(rb, W);
-    if (act && rb.valid < 64) {
-      pad_words_lane(rb.valid, W);
-      if (jb.fin && blk + 1 == jb.nblocks) {
-        const uint64_t bits = (jb.consumed + jb.L) * 8ull;
-        W[14] = (uint32_t)(bits >> 32);
-        W[15] = (uint32_t)bits;
-      }
-    }
-  } else {
-    sha_load_slow(jb, blk, W);  // head block of a continued chunk (once per segment)
-  }
 }
 
-// A region's pop counter holds two counts (round 5, BSG_LANE_YOUNG): the jobs taken from its
-// head (longest first, waves 0-3) in the low word, those taken from its tail (shortest first,
-// the young waves 4-7) in the high word; the jobs left are rorder[off + hd .. off + n - tl).
-// Returns hd, or n when no job is left.
+// A region's pop counter: the jobs taken from it so far (longest first); the jobs left are
+// rorder[off + hd .. off + n). Returns hd, or n when no job is left.
 __device__ __forceinline__ uint64_t reg_head(const ShaArgs& a, uint32_t r, uint64_t n) {
-  const uint64_t v = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t hd = (uint32_t)v, tl = v >> 32;
-  return hd + tl < n ? hd : n;
+  const uint64_t hd =
+      __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return hd < n ? hd : n;
 }
 
 // The region whose next job is the longest (longest-first across regions, so the last jobs
@@ -1620,54 +1157,6 @@ __device__ uint32_t pick_region(const ShaArgs& a, uint32_t R, uint32_t start) {
 #ifndef BSG_REGION_POLL
 #define BSG_REGION_POLL 8      // a wave compares its region's progress with the others' every
 #endif                         // this many pops (0: only when its region runs dry)
-#ifndef BSG_REGION_LAG
-#define BSG_REGION_LAG 3       // BSG_REGION_BY_LEN=0 only: ... and moves if it is this many % of
-#endif                         // its jobs ahead of the region furthest behind
-
-// (Round-2 poll, kept for BSG_REGION_BY_LEN=0.) Regions are drained longest job first, so the
-// share of a region's jobs already taken says how far down its length order it is (but not how
-// long its next job is). Returns the region furthest behind if `cur` is more than
-// BSG_REGION_LAG % ahead of it, else `cur`. One round of loads; called by a whole wave.
-__device__ uint32_t behind_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
-  const uint64_t act = __ballot(1);
-  const uint32_t nact = (uint32_t)__popcll(act);
-  const uint32_t rank =
-      __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-  uint64_t key = 0;       // (2^20 - share taken) << 8 | (255 - distance from cur)
-  uint32_t mine = 0;      // cur's share taken (2^20 = all), on the lane that read it
-  bool has_mine = false;
-  for (uint32_t r = rank; r < R; r += nact) {
-    const uint64_t o = a.reg->off[r], n = a.reg->off[r + 1] - o;
-    const uint64_t h = reg_head(a, r, n);
-    const uint32_t taken = n ? (uint32_t)(min(h, n) * (1ull << 20) / n) : (1u << 20);
-    if (r == cur) {
-      mine = taken;
-      has_mine = true;
-    }
-    if (h < n) {
-      const uint64_t k = ((uint64_t)((1u << 20) - taken) << 8) | (255u - (r + R - cur) % R);
-      key = k > key ? k : key;
-    }
-  }
-  uint64_t best = 0;
-  uint32_t cur_taken = 0;
-  for (uint64_t m = act; m; m &= m - 1) {
-    const int l = (int)__builtin_ctzll(m);
-    const uint64_t v =
-        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), l) << 32) |
-        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, l);
-    best = v > best ? v : best;
-    if (__builtin_amdgcn_readlane((int)has_mine, l)) cur_taken = (uint32_t)__builtin_amdgcn_readlane((int)mine, l);
-  }
-  if (!best) return cur;
-  const uint32_t behind_taken = (1u << 20) - (uint32_t)(best >> 8);
-  if (cur_taken <= behind_taken + (uint32_t)(((1ull << 20) * BSG_REGION_LAG) / 100)) return cur;
-  return (cur + 255u - (uint32_t)(best & 255u)) % R;
-}
-
-#ifndef BSG_REGION_BY_LEN
-#define BSG_REGION_BY_LEN 1    // poll by next-job length (0: by share taken, behind_region)
-#endif
 #ifndef BSG_REGION_LEN_LAG
 #define BSG_REGION_LEN_LAG 25  // ... moving if another region's next job is this many % longer
 #endif
@@ -1715,7 +1204,7 @@ __device__ uint32_t longer_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
 }
 
 // Per-lane mode: each lane hashes one chunk at a time, longest first within the address region
-// its wave works on (Regions). An iteration hashes BSG_LANE_BPI blocks per lane. Starting the
+// its wave works on (Regions). An iteration hashes kLaneBPI blocks per lane. Starting the
 // next job is pipelined per lane, one memory step per iteration, so no iteration waits for
 // more than what the one before issued:
 //   BSG_LANE_LEAD iterations before its job ends a lane pops a slot of its wave's region
@@ -1727,13 +1216,10 @@ __device__ uint32_t longer_region(const ShaArgs& a, uint32_t R, uint32_t cur) {
 // one ended, and the whole wave waited for that atomic and ~4 dependent loads whenever any
 // lane switched. A job too short for the pipeline idles only its own lane until its successor
 // is ready; continued and open chunks (streaming) still take the synchronous sha_setup path.
-// young (BSG_LANE_YOUNG, waves 4-7 of a k_sha workgroup): the wave shares its SIMD with an older
-// one, which the SIMD serves first, so it runs at about half speed (tools/ubench/lanes_align.hip,
-// profiles/r05_lanes_prio.log: 11,300 against 5,700 cycles per block, the older wave unslowed).
-// It takes its region's jobs from the tail, shortest first, never a long one that would end
-// late, and does not chase other regions' longest jobs (no poll).
-__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) {
-  constexpr int kBPI = BSG_LANE_BPI;  // blocks per iteration (per lane)
+// The compressions are one generated asm statement (sha256_compress_kv, sha256_lane_asm.inc)
+// with K in 64 resident VGPRs: k_sha runs one wave per SIMD, so it has VGPRs to spare.
+__device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
+  constexpr int kBPI = kLaneBPI;  // blocks per iteration (per lane)
   const uint32_t lane = threadIdx.x & 63u;
   ShaJob jb;
   jb.dbase = a.data;  // a readable address for the idle prefetch before the first job
@@ -1743,10 +1229,8 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
   jb.nblocks = 0;
   jb.fin = 1;
   uint32_t st[8] = {};
-#if BSG_LANE_ASM == 2
-  uint32_t kv[64];  // K, resident for the whole loop (k_sha has one wave per SIMD: VGPRs to spare)
+  uint32_t kv[64];  // K, resident for the whole loop
   sha256_k_regs(kv);
-#endif
   RawBlock rb[kBPI];
 #pragma unroll
   for (int b = 0; b < kBPI; ++b) {
@@ -1783,19 +1267,11 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
   bool all_done = false;
   uint32_t npops = 0;     // pops by this wave (wave-uniform)
   bool poll = false;
-  LANE_DIAG_INIT
   for (;;) {
-    LANE_DIAG_ITER(act)
     // Everything the last iteration issued (block prefetch, pipeline loads, the pop, the
     // record store) has had a whole compression to land: wait for all of it here, once, so
     // the compiler needs no wait further down.
-#if BSG_LANE_DIAG
-    const uint64_t d_w0 = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
-    d_wait += __builtin_amdgcn_s_memtime() - d_w0;
-#else
-    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
-#endif
     uint32_t W[kBPI][16];
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)  // garbage on idle lanes and past a job's end (never used)
@@ -1812,12 +1288,11 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
       nj_d = nj;  // its descriptor is loaded below
       stage = 5;
     } else if (stage == 1) {
+      // the region's pop count before this pop (a region holds < 2^32 jobs)
       const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pop_base, pop_leader);
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pop_base >> 32), pop_leader);
-      // the counts before this pop: lo from the head, hi from the tail (reg_head)
-      const uint64_t local = (uint64_t)(young ? hi : lo) + pop_rank;
-      dry = local + (young ? lo : hi) >= pop_n;
-      q = young ? pop_off + pop_n - 1 - local : pop_off + local;
+      const uint64_t local = (uint64_t)lo + pop_rank;
+      dry = local >= pop_n;
+      q = pop_off + local;
       stage = dry ? 0u : 2u;  // its job id is loaded below; else the region ran dry
     }
     }
@@ -1825,7 +1300,6 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
       // the current region ran dry: move to the one with the most jobs left (wave-uniform,
       // synchronous; a few times per wave)
       reg = pick_region(a, R, reg + 1);
-      d_moves += 1;
       if (reg >= R) {
         all_done = true;
       } else {
@@ -1833,15 +1307,15 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
         reg_n = a.reg->off[reg + 1] - reg_off;
       }
     }
-    if (BSG_REGION_POLL && poll && !all_done && R > 1 && !young) {
-      // keep the regions level: move to the one furthest behind if this one is well ahead
+    if (BSG_REGION_POLL && poll && !all_done && R > 1) {
+      // keep the waves on one global longest-first order: move to the region whose next job is
+      // well longer than this one's
       poll = false;
-      const uint32_t r2 = BSG_REGION_BY_LEN ? longer_region(a, R, reg) : behind_region(a, R, reg);
+      const uint32_t r2 = longer_region(a, R, reg);
       if (r2 != reg) {
         reg = r2;
         reg_off = a.reg->off[reg];
         reg_n = a.reg->off[reg + 1] - reg_off;
-        d_moves += 1;
       }
     }
     const bool ld_ready = stage == 3;
@@ -1869,7 +1343,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
         uint32_t z;
         asm volatile("v_mov_b32 %0, 0" : "=v"(z));
         pop_base = atomicAdd(reinterpret_cast<unsigned long long*>(&a.reg->head[reg]) + z,
-                             (unsigned long long)__popcll(nm) << (young ? 32 : 0));
+                             (unsigned long long)__popcll(nm));
       }
       pop_leader = leader;
       pop_off = reg_off;
@@ -1900,34 +1374,15 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
     const uint64_t ld_start = ((uint64_t)ld0.w << 32) | ld0.z;
     const uint64_t ld_len = ((uint64_t)ld1.y << 32) | ld1.x;
     const bool take = !cont && ld_ready && !(ld1.w & kLaneJobSlow);
-#ifndef BSG_LANE_LOADN
-#define BSG_LANE_LOADN 1
-#endif
-#if BSG_LANE_LOADN
-    {
+    {  // both blocks of the iteration from one aligned base and byte selector (raw_load_n)
       const uint64_t o0 = take ? 0ull : 64ull * (blk + kBPI);
       const uint8_t* p0 = take ? reinterpret_cast<const uint8_t*>(ld_dptr)
                                : jb.dbase + (o0 - jb.prefix);
       raw_load_n<kBPI>(p0, o0, take ? ld_len : jb.L, rb);
     }
-#else
 #pragma unroll
     for (int b = 0; b < kBPI; ++b)
-      raw_load(take ? reinterpret_cast<const uint8_t*>(ld_dptr) : jb.dbase,
-               take ? 64ull * b : 64ull * (blk + kBPI + b), take ? 0u : jb.prefix,
-               take ? ld_len : jb.L, rb[b]);
-#endif
-#pragma unroll
-    for (int b = 0; b < kBPI; ++b)
-      if (act && blk + b < jb.nblocks) {
-#if BSG_LANE_ASM == 2
-        sha256_compress_kv(st, W[b], kv);
-#elif BSG_LANE_ASM
-        sha256_compress_aligned(st, W[b]);
-#else
-        sha256_compress(st, W[b]);
-#endif
-      }
+      if (act && blk + b < jb.nblocks) sha256_compress_kv(st, W[b], kv);
     blk += kBPI;
     if (LANE_ANY(act && blk >= jb.nblocks) && act && blk >= jb.nblocks) {
       act = false;
@@ -1943,7 +1398,7 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
       } else {
         sha_finish(a, jb, st);  // open chunk: midstate carry (streaming, one per stream)
       }
-      if (stamp && !BSG_LANE_DIAG) {
+      if (stamp) {
         a.ctr->diag2[1] = __builtin_amdgcn_s_memtime();
         a.ctr->diag2[3] = __builtin_amdgcn_s_memrealtime();
         a.ctr->diag2[0] = tm0;
@@ -1993,7 +1448,6 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M, bool young = false) 
       }
     }
   }
-  LANE_DIAG_END
 }
 
 
@@ -2293,7 +1747,7 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(ShaArgs a) {
     a.ctr->nlong_grp = n8;
     a.ctr->tickets_grp = t8;
     // lightly loaded: the solo tickets run with helper waves (k_sha<true>), the queue after them
-    const uint64_t helped = (BSG_HELP_SOLO && BSG_SHA_WAVES == 4 && light && a.long_mode == 0)
+    const uint64_t helped = (light && a.long_mode == 0)
                                 ? min(min((uint64_t)n8, (uint64_t)kSolo), (uint64_t)a.waves / 2)
                                 : 0;
     a.ctr->helped = helped;
@@ -2432,10 +1886,6 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     tr0 = __builtin_amdgcn_s_memrealtime();
   }
   const uint32_t nmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
-#if BSG_LANE_DIAG
-  const uint64_t d_tk0 = __builtin_amdgcn_s_memrealtime();
-#endif
-#if BSG_BANK_ROUNDS
   // Pair tickets: skewed lane pairs (2p: E, 2p+1: A). Solo and group tickets: skewed octets
   // (one chain per 8 lanes, E quad at positions 0-3, A quad at 4-7; 8 VALU per round against
   // the pair's 9). Half states A: H0..H3, E: H6, H7, H4, H5.
@@ -2447,7 +1897,6 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   hs[1] = a_side ? st[1] : st[7];
   hs[2] = a_side ? st[2] : st[4];
   hs[3] = a_side ? st[3] : st[5];
-#endif
   // Each ring fill's message block is requested one fill ahead, before the chain runs on the
   // current fill, so a fill never waits for HBM (a pair ticket fills every 2 blocks).
   RawBlock rb;
@@ -2488,7 +1937,6 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
     ring_sync();
     // phase B: blocks base .. base+B-1 of every chain
     const uint32_t steps = min(B, nmax - base);
-#if BSG_BANK_ROUNDS
     const uint32_t* ones = ring + 64 * kLongRow;
     const uint32_t* krow = a_side ? ones : ring + cR * B * kLongRow;
     const uint32_t stride = a_side ? 0u : 4u * kLongRow;
@@ -2496,27 +1944,8 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
       sha256_blocks_skew(hs, krow, stride, steps, (int32_t)nb - (int32_t)base, bl);
     else
       sha256_blocks_oct(hs, krow, stride, steps, (int32_t)nb - (int32_t)base, ol);
-#else
-    for (uint32_t i = 0; i < steps; ++i) {
-      const u32x4a* r = reinterpret_cast<const u32x4a*>(ring + (cR * B + i) * kLongRow);
-      uint32_t KW[64];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const u32x4a v = r[q];
-        KW[4 * q] = v.x; KW[4 * q + 1] = v.y; KW[4 * q + 2] = v.z; KW[4 * q + 3] = v.w;
-      }
-      uint32_t s2[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s2[k] = st[k];
-      sha256_rounds_kw<true>(s2, KW);
-      const bool act = base + i < nb;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) st[k] = act ? s2[k] : st[k];
-    }
-#endif
     ring_sync();
   }
-#if BSG_BANK_ROUNDS
   // each lane collects its chain's state: H0..H3 from an A lane (the pair's odd lane, the
   // octet's position 4), H4..H7 from its E lane
   const int pe = (int)(lane & ~(B - 1u)), pa = (int)((lane & ~(B - 1u)) | (pairs ? 1u : 4u));
@@ -2526,19 +1955,6 @@ __device__ void sha_wave_job(const ShaArgs& a, uint64_t M, uint64_t t, uint64_t 
   st[7] = (uint32_t)__shfl((int)hs[1], pe);
   st[4] = (uint32_t)__shfl((int)hs[2], pe);
   st[5] = (uint32_t)__shfl((int)hs[3], pe);
-#endif
-#if BSG_LANE_DIAG
-  {
-    const uint32_t wid = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && wid < 1024) {
-      a.reg->wdbg[8 * wid + 4] = t + 1;
-      a.reg->wdbg[8 * wid + 5] = d_tk0;
-      a.reg->wdbg[8 * wid + 6] = rt1;
-      a.reg->wdbg[8 * wid + 7] = (uint64_t)nmax | ((uint64_t)(solo ? 0 : pairs ? 2 : 1) << 32);
-    }
-  }
-#endif
   if (vb && (lane & (B - 1u)) == 0) {
     sha_finish(a, jb, st);
     if (stamp) {
@@ -2564,7 +1980,7 @@ __device__ __forceinline__ uint64_t pop_uniform(uint64_t* head) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Solo tickets of a lightly loaded launch, with a helper wave (BSG_HELP_SOLO). A solo chain's
+// Solo tickets of a lightly loaded launch, with a helper wave. A solo chain's
 // wave otherwise stops every 64 blocks to expand the next 64 message schedules into its ring:
 // ~50 of its ~2,720 cycles per block, on the launch's critical path. Here the first workgroups
 // to start (k_sha<true>) take solo tickets in pairs: waves 0 and 1 run the two chains, waves 2
@@ -2729,26 +2145,13 @@ __device__ void sha_solo_fill(const ShaArgs& a, uint64_t M, uint64_t t, uint32_t
 // wave-instruction; a second wave on the SIMD only runs in the first one's gaps), so stacking
 // waves gains nothing and would stall the latency-critical wave-mode chains. Every wave first
 // drains the long-job queue in wave mode, then turns to per-lane mode (longest-first order).
-constexpr uint32_t kShaWaves = BSG_SHA_WAVES;
-static_assert(kShaWaves == 4 || kShaWaves == 8, "4 chain-capable waves per workgroup (+4 lane-only)");
-// BSG_LANE_YOUNG (round 5): four more waves per workgroup, one more per SIMD, in per-lane mode
-// only, taking each region's shortest jobs (sha_lane_mode's `young`). The SIMD serves the older
-// wave first, so waves 0-3 (chains, the longest per-lane jobs) keep their lone-wave speed and
-// the young ones fill the issue slots they leave (profiles/r05_lanes_prio.log: together 1.5x the
-// per-lane blocks of one wave). Round 2's eight-wave forms gave the longest per-lane jobs to
-// waves that shared a SIMD.
-// Measured (profiles/r05_ab21_*.log): configs[2] 886-902 against 914-970 GiB/s. The chains
-// slowed by ~4 % beside the young waves (long_end 12.27 against 11.80 ms) at the same cycles per
-// block (2,333-2,336 against 2,330-2,336): the clock fell, 2.23-2.24 against 2.32-2.34 GHz, so the
-// extra issue costs the chip power, not the chains' issue slots. And the young waves'
-// last jobs, taken where the two ends of a region meet, were medium ones at half speed
-// (lane_end 13.8 against 12.6 ms); the per-lane work is mostly in the long jobs, so a young wave
-// held to short ones adds little. Off.
-#ifndef BSG_LANE_YOUNG
-#define BSG_LANE_YOUNG 0
-#endif
-static_assert(!BSG_LANE_YOUNG || kShaWaves == 4, "young waves join the four chain-capable ones");
-constexpr uint32_t kShaBlock = 64 * (kShaWaves + (BSG_LANE_YOUNG ? 4 : 0));
+// (Measured and dropped: 8 waves per workgroup, two per SIMD — the chains kept their speed but
+// the longest per-lane jobs, sharing a SIMD, took 1.5x as long (round 2); and four more per-lane
+// waves taking each region's shortest jobs beside waves 0-3 (round 5, profiles/r05_ab21_*.log:
+// configs[2] 886-902 against 914-970 GiB/s; the chip's clock fell from 2.32-2.34 to 2.23-2.24 GHz
+// under the extra issue, slowing the chains by 4 % at the same cycles per block).)
+constexpr uint32_t kShaWaves = 4;
+constexpr uint32_t kShaBlock = 64 * kShaWaves;
 
 // Two instantiations, launched back to back; the one that does not match the launch (helped
 // solo tickets or not, k_bucket_scan) returns at once. k_sha<false> holds no helper code, so
@@ -2770,14 +2173,7 @@ __global__ __launch_bounds__(kShaBlock, 1) void k_sha(ShaArgs a) {
   }
   const uint64_t ntickets = a.ctr->ntickets;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // BSG_SHA_WAVES=8 (experiment): the first ceil(tickets / 4) workgroups take
-  // the wave-mode tickets on waves 0-3 (waves 4-7 leave at once, so no chain shares its SIMD);
-  // every other workgroup runs per-lane mode on all 8 waves, two per SIMD. The chains kept
-  // their speed, but the longest per-lane jobs, now sharing a SIMD, took 1.5x as long.
-  const bool chain_wg = kShaWaves == 4 || (uint64_t)blockIdx.x * 4 < ntickets;
-  if (kShaWaves > 4 && chain_wg && wv >= 4) return;
-  const bool young = BSG_LANE_YOUNG && wv >= 4;  // (takes part in the workgroup's barriers)
-  uint32_t* ring = lds + (wv & 3u) * kRingWords;
+  uint32_t* ring = lds + wv * kRingWords;
   uint64_t t = ~0ull;
   bool helper_wg = false;
   if constexpr (HELP) {  // the first workgroups to start take the helped solo pairs
@@ -2792,7 +2188,7 @@ __global__ __launch_bounds__(kShaBlock, 1) void k_sha(ShaArgs a) {
       __syncthreads();
       const uint32_t c = wv & 1u;
       const uint64_t ht = hw * 2 + c;
-      if (ht < helped && !young) {
+      if (ht < helped) {
         __builtin_amdgcn_s_setprio(3);
         if (wv < 2) sha_solo_chain(a, M, ht, lds, c);
         else sha_solo_fill(a, M, ht, lds, c);
@@ -2800,7 +2196,7 @@ __global__ __launch_bounds__(kShaBlock, 1) void k_sha(ShaArgs a) {
       }
     }
   }
-  if (chain_wg && !helper_wg && !young) {
+  if (!helper_wg) {
     // row of ones after each wave's 64 K+W rows (the A lanes' kw in sha256_rounds_bank)
     for (uint32_t i = threadIdx.x & 63u; i < (uint32_t)kLongRow; i += 64) ring[64 * kLongRow + i] = 1u;
     // A plain pre-tested loop on a scalar ticket: a `for (;;) { if (lane == 0) atomic; ...;
@@ -2818,7 +2214,7 @@ __global__ __launch_bounds__(kShaBlock, 1) void k_sha(ShaArgs a) {
     }
     __builtin_amdgcn_s_setprio(0);
   }
-  sha_lane_mode(a, M, young);
+  sha_lane_mode(a, M);
   if ((threadIdx.x & 63u) == 0)
     atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->lane_end_rt),
               (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -3003,11 +2399,7 @@ __global__ __launch_bounds__(256) void k_sha_blobs(BlobShaArgs a) {
         }
       }
       raw_load(jb.dbase, 64ull * (blk + 1), 0, jb.L, rb);
-#if BSG_LANE_ASM
       sha256_compress_aligned(st, W);
-#else
-      sha256_compress(st, W);
-#endif
     }
     uint32_t* ref = reinterpret_cast<uint32_t*>(a.refs + 32 * i);
 #pragma unroll
@@ -3050,19 +2442,15 @@ static inline uint32_t grid_for(uint64_t items, uint32_t per_block, uint32_t cap
   return (uint32_t)(g < cap ? g : cap);
 }
 
-#ifndef BSG_SCAN_GRID
-#define BSG_SCAN_GRID 2  // k_scan workgroups per CU in the grid (one is resident at a time)
-#endif
 uint32_t scan_lists(uint64_t nstrips, int num_cus) {
   const uint64_t groups = (nstrips + kScanGroup - 1) / kScanGroup;
-  const uint32_t per_cu = BSG_SCAN_DYN ? 1u : (uint32_t)BSG_SCAN_GRID;
-  return grid_for(groups, 1, per_cu * (kScanPair ? 2u : 1u) * (uint32_t)num_cus);
+  return grid_for(groups, 1, 2u * (uint32_t)num_cus);  // two k_scan workgroups per CU
 }
 
 uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists) {
   const uint64_t groups = (nstrips + kScanGroup - 1) / kScanGroup;
   const uint64_t share = lists ? (groups + lists - 1) / lists : 0;
-  return (BSG_SCAN_DYN ? min(groups, kScanDynShare * share) : share) * (uint64_t)kScanGroup;
+  return min(groups, kScanDynShare * share) * (uint64_t)kScanGroup;
 }
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
@@ -3076,62 +2464,26 @@ hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus) {
   return hipGetLastError();
 }
 
-// The refine-list consumers: one workgroup per list (BSG_SCAN_WGLIST), else a grid-stride walk.
-static uint32_t refine_grid(const ScanArgs& a, uint32_t per_wg, uint32_t cap) {
-#if BSG_SCAN_WGLIST
-  (void)per_wg;
-  (void)cap;
-  return a.lists;
-#else
-  return grid_for(a.nstrips, per_wg, cap);
-#endif
-}
-
-hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus) {
-#if BSG_SCAN_FUSE && BSG_SCAN_WGLIST
-  (void)a;
-  (void)s;
-  (void)num_cus;
-  return hipSuccess;  // k_scan did it
-#endif
-  const uint32_t grid = refine_grid(a, (uint32_t)kScanWG, 2u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_refine, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4 + kStrip0Lds * 8, s, a);
+// The refine-list consumers run one workgroup per k_scan workgroup's list.
+hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int) {
+  hipLaunchKernelGGL(k_compact, dim3(a.lists), dim3(256), kStrip0Lds * 8, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus) {
-  const uint32_t cgrid = refine_grid(a, 256, 16u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_compact, dim3(cgrid), dim3(256), kStrip0Lds * 8, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_rescan(const ScanArgs& a, hipStream_t s, int num_cus) {
-  const uint32_t grid = refine_grid(a, (uint32_t)kScanWG, 2u * (uint32_t)num_cus);
-  hipLaunchKernelGGL(k_rescan, dim3(grid), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
+hipError_t launch_rescan(const ScanArgs& a, hipStream_t s, int) {
+  hipLaunchKernelGGL(k_rescan, dim3(a.lists), dim3(kScanWG), kTabRows * kTabRep * 4, s, a);
   return hipGetLastError();
 }
 
 uint64_t prefix_partials_needed(uint64_t n_bound) {
-  return (n_bound + kScanTile - 1) / kScanTile + 2;  // tiles (at least one), then the ticket
+  const uint64_t nb = (n_bound + kScanTile - 1) / kScanTile;
+  return nb ? nb : 1;  // a status word per tile (an empty input still runs tile 0)
 }
 
-#ifndef BSG_PREFIX1
-#define BSG_PREFIX1 1  // the single-pass prefix (0: three kernels, round 4)
-#endif
 hipError_t launch_prefix(const PrefixArgs& a, hipStream_t s) {
-  const uint64_t nb = (a.n_bound + kScanTile - 1) / kScanTile;
-#if BSG_PREFIX1
-  // status words [0, nb) and the ticket at [nb], zeroed by k_start (prefix_partials_needed)
-  hipLaunchKernelGGL(k_prefix1, dim3((uint32_t)(nb ? nb : 1)), dim3(kScanT), 0, s, a, nb ? nb : 1);
-  return hipGetLastError();
-#endif
-  if (nb == 0) {
-    hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(1024), 0, s, a, (uint64_t)0);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(k_prefix_reduce, dim3((uint32_t)nb), dim3(kScanT), 0, s, a);
-  hipLaunchKernelGGL(k_prefix_top, dim3(1), dim3(1024), 0, s, a, nb);
-  hipLaunchKernelGGL(k_prefix_down, dim3((uint32_t)nb), dim3(kScanT), 0, s, a);
+  // status words [0, nb), zeroed by k_start (prefix_partials_needed)
+  const uint64_t nb = prefix_partials_needed(a.n_bound);
+  hipLaunchKernelGGL(k_prefix1, dim3((uint32_t)nb), dim3(kScanT), 0, s, a);
   return hipGetLastError();
 }
 

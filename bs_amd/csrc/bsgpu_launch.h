@@ -16,9 +16,9 @@ struct ScanArgs {
   const uint32_t* table;    // 256 buzhash32 entries
   Params p;
   uint32_t* counts;         // [nstrips]
-  uint64_t* refine;         // [lists * list_cap] strips k_refine must scan exactly: strip << 32 |
-                            // the fast pass's hit mask (one bit per 64-byte block); k_scan
-                            // workgroup g appends to refine + g * list_cap (BSG_SCAN_WGLIST)
+  uint64_t* refine;         // [lists * list_cap] strips k_scan's exact pass must scan: strip << 32
+                            // | the fast pass's hit mask (one bit per 64-byte block); k_scan
+                            // workgroup g appends to refine + g * list_cap
   uint32_t* slots;          // [nstrips * kSlotCap]
   const uint64_t* cand_off; // [nstrips] exclusive candidate offsets (compact)
   uint64_t* cand;           // [cand_cap]
@@ -27,9 +27,8 @@ struct ScanArgs {
   uint32_t lists;           // k_scan's grid = the number of refine lists (scan_lists())
   uint64_t list_cap;        // entries per list: the strips one k_scan workgroup scans, at most
   uint32_t* list_cnt;       // [lists] each list's length, stored by its workgroup at exit
-  uint64_t* dbg;            // BSG_SCAN_DIAG builds: k_scan's phase stamps (else null)
 };
-// k_scan's grid for nstrips strips (its workgroups loop over 512-strip groups) and the length
+// k_scan's grid for nstrips strips (its workgroups take 256-strip groups by ticket) and the length
 // bound of each workgroup's refine list; the host sizes ScanArgs::refine with them.
 uint32_t scan_lists(uint64_t nstrips, int num_cus);
 uint64_t scan_list_cap(uint64_t nstrips, uint32_t lists);
@@ -134,7 +133,6 @@ struct BlobShaArgs {
 };
 
 hipError_t launch_scan(const ScanArgs& a, hipStream_t s, int num_cus);
-hipError_t launch_refine(const ScanArgs& a, hipStream_t s, int num_cus);
 hipError_t launch_compact(const ScanArgs& a, hipStream_t s, int num_cus);
 hipError_t launch_rescan(const ScanArgs& a, hipStream_t s, int num_cus);
 uint64_t prefix_partials_needed(uint64_t n_bound);

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstddef>
+#include <cstdint>
 #include <functional>
 
 namespace bsg {
@@ -17,5 +18,19 @@ int copy_threads();
 // Runs fn(i) for every i in [0, n) on the pool and on the calling thread, and returns when all
 // have run. fn must not call parallel_for itself.
 void parallel_for(size_t n, const std::function<void(size_t)>& fn);
+
+// Copies of Write bytes into buffers nobody reads soon from the CPU (pinned stages the DMA engine
+// reads, Write pieces a store keeps): non-temporal stores (BSG_KNOB_COPY_NT, default on), so the
+// destination lines are written without first being read into the cache. A plain memcpy reads
+// every destination line before writing it: on the staging path that is 4 passes over host
+// memory per byte (source read, stage read + written back, DMA read), this is 3.
+void copy_nt(uint8_t* dst, const uint8_t* src, size_t n);
+// One read of src feeding two destinations (the Writer's piece and the pinned stage): 3 passes
+// over host memory per byte instead of 5 for two memcpys (piece read+written, stage read+written,
+// and the DMA read aside).
+void copy_nt2(uint8_t* d1, uint8_t* d2, const uint8_t* src, size_t n);
+bool copy_nt_enabled();
+// NUMA node of the CPU the calling thread runs on (-1 unknown)
+int cpu_node();
 
 }  // namespace bsg

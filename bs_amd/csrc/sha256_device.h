@@ -12,19 +12,10 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t r) {
   return __builtin_amdgcn_alignbit(x, x, r);
 }
 // 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); hipcc emits two v_xor
-// for a ^ b ^ c. BSG_BITOP3_ASM=1 uses inline asm (round 1); by default the compiler builtin,
-// which the scheduler can move like any other instruction.
-#ifndef BSG_BITOP3_ASM
-#define BSG_BITOP3_ASM 0
-#endif
+// for a ^ b ^ c. The compiler builtin, which the scheduler can move like any other instruction
+// (round 1 used inline asm).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-#if BSG_BITOP3_ASM
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-#else
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -43,13 +34,7 @@ static constexpr uint32_t kK256[64] = {
 template <uint32_t TT>
 __device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
   // v_bitop3_b32: bit i of the result = TT[(a_i << 2) | (b_i << 1) | c_i]
-#if BSG_BITOP3_ASM
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
-  return r;
-#else
   return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
-#endif
 }
 
 // One SHA-256 round, 14 VALU ops: 3+1 (Sigma1), Ch (bitop3 0xCA), h+K+W, add3, d += T1,
@@ -99,7 +84,8 @@ __device__ __forceinline__ void sha256_compress(uint32_t (&st)[8], uint32_t (&W)
 // 8-byte encodings with about half its 8-byte instructions at 4 mod 8, and takes 235 VGPRs in
 // k_sha against 188 with this one. A lone wave runs both at ~6,000 cycles per block
 // (profiles/r05_lanes_align.log); in k_sha under the configs[2] load the asm form takes k_sha
-// from 13.44 to 13.10 ms (profiles/r05_ab8.log). k_sha's per-lane mode uses it (BSG_LANE_ASM).
+// from 13.44 to 13.10 ms (profiles/r05_ab8.log). k_sha_blobs uses it; k_sha's per-lane mode
+// uses sha256_compress_kv below (K from resident VGPRs).
 #include "sha256_lane_asm.inc"
 __device__ __forceinline__ void sha256_compress_aligned(uint32_t (&st)[8], uint32_t (&W)[16]) {
   uint32_t x0, x1, x2, x3, x4, x5, x6, x7, t0, t1, t2, t3, t4, t5, k;

@@ -312,9 +312,24 @@ class Writer {
   // (drain: records processed on the background thread, overlapping the copies; join: what the
   // Writes waited for it)
   struct Timing {
-    double copy = 0, drain = 0, join = 0, hash = 0, close = 0;
+    double copy = 0, drain = 0, join = 0, hash = 0, close = 0, close_dev = 0;
     uint64_t hash_calls = 0;
   } tm_;
+
+ public:
+  // tm_ in seconds: [0] Write copies, [1] records processed on the background thread (Put +
+  // TreeBuilder.Add, overlapping the copies), [2] Writes and Close waiting for that thread,
+  // [3] tree-node hashes (GPU), [4] Close, [5] of which waiting for the last tiles on the device,
+  // [6] tree-node hash calls
+  void Timings(double out[7]) const {
+    out[0] = tm_.copy;
+    out[1] = tm_.drain;
+    out[2] = tm_.join;
+    out[3] = tm_.hash;
+    out[4] = tm_.close;
+    out[5] = tm_.close_dev;
+    out[6] = (double)tm_.hash_calls;
+  }
 };
 
 // split.Protect (split/split.go:306-322), the gc.ProtectFunc for split trees: the children of

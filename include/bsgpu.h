@@ -133,6 +133,27 @@ int bsg_set_stream_base(bsg_ctx* ctx, uint64_t base);
  * pool of split.Writers would; undrained chunks of the previous stream are discarded. */
 int bsg_reset(bsg_ctx* ctx);
 void bsg_free(bsg_ctx* ctx);
+/* Where a stream's host-to-device time went, since bsg_open / the last bsg_reset (a diagnostic:
+ * an io.Copy into split.Writer is bound by the host copy, the PCIe copy or the device). Waits
+ * for the context's copy stream. */
+typedef struct bsg_stream_stats {
+  uint64_t host_bytes;         /* bytes bsg_write copied into pinned staging */
+  uint64_t host_copy_ns;       /* wall time of those copies (all copy threads together) */
+  uint64_t stage_wait_ns;      /* time Writes waited for a stage's previous H2D copy */
+  uint64_t h2d_bytes;          /* bytes copied host-to-device from the stages */
+  uint64_t h2d_copies;         /* number of those copies */
+  uint64_t h2d_busy_ns;        /* sum of their durations (HIP events on the copy stream) */
+  uint64_t h2d_span_ns;        /* the first one's start to the last one's end */
+  uint64_t copy_bytes_node[4]; /* host copy bytes by NUMA node of the copying thread's CPU */
+  uint64_t last_tile_ns;       /* the final tile's kernels on the device (bsg_close's tail) */
+  uint64_t tail_ns;            /* the last H2D copy's end to the final tile's records in host
+                                * memory */
+  int32_t gpu_node;            /* NUMA node of the device (sysfs; -1 unknown) */
+  uint32_t stage_nodes;        /* bit mask of the NUMA nodes the pinned stages' pages are on */
+  uint32_t src_nodes;          /* bit mask of the nodes of the Write sources' first pages */
+  uint32_t copy_nt;            /* 1: the copies used non-temporal stores */
+} bsg_stream_stats;
+int bsg_stream_stats_get(bsg_ctx* ctx, bsg_stream_stats* out);
 
 /* ---- device-resident batch of independent streams ---- */
 typedef struct bsg_engine bsg_engine;
@@ -272,6 +293,12 @@ int bsg_writer_close(bsg_writer* w);
  * Writer's tree and Root are unchanged (tree offsets start at 0, as split.Writer's). */
 int bsg_writer_set_stream_base(bsg_writer* w, uint64_t base);
 int bsg_writer_root(const bsg_writer* w, uint8_t out[32]);
+/* Where the Writer's time went, in seconds: [0] Write copies (into its pieces and pinned
+ * staging), [1] chunk records processed on its background thread (store Puts + the tree,
+ * overlapping the copies), [2] Writes and Close waiting for that thread, [3] tree-node hashes
+ * on the GPU, [4] Close, [5] of which waiting for the last tiles on the device, [6] tree-node
+ * hash calls. */
+int bsg_writer_timings(const bsg_writer* w, double out[7]);
 void bsg_writer_free(bsg_writer* w);
 
 typedef struct bsg_reader bsg_reader; /* split.NewReader / Read / Seek / Size */
@@ -301,9 +328,14 @@ void bsg_reader_free(bsg_reader* r);
 #define BSG_KNOB_EARLY 4         /* BSG_EARLY: 1 (default) hashes the two longest chunks whose
                                   * ends are sure boundaries on a second stream from right after
                                   * candidate compaction (engine runs of >= 256 MiB); 0 off */
-#define BSG_KNOB_POLL 5          /* BSG_POLL: 1 makes bsg_engine_finish wait by polling its
-                                  * stream (one host core busy for the run, no interrupt wake-up
-                                  * latency); 0 (default) blocks in hipStreamSynchronize */
+#define BSG_KNOB_POLL 5          /* BSG_POLL: 1 (default) makes bsg_engine_finish poll its stream
+                                  * (with a CPU pause between queries, for at most 100 ms, then it
+                                  * blocks: no interrupt wake-up latency on a step-sized run); 0
+                                  * blocks in hipStreamSynchronize at once */
+#define BSG_KNOB_COPY_NT 6       /* BSG_COPY_NT: 1 (default) copies Write bytes into pinned
+                                  * staging (and the Writer's pieces) with non-temporal stores;
+                                  * 0 uses memcpy */
+#define BSG_KNOB_LAST BSG_KNOB_COPY_NT
 int bsg_debug_set(int knob, int64_t value);
 int64_t bsg_debug_get(int knob); /* -1 for an unknown knob */
 
