@@ -217,7 +217,8 @@ def _p(a: np.ndarray, ct):
 
 
 # bsg_debug_set
-KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY, KNOB_POLL, KNOB_COPY_NT = range(1, 7)
+(KNOB_SEQ_WAIT, KNOB_LONG_MODE, KNOB_VERIFY_WINDOW, KNOB_EARLY, KNOB_POLL, KNOB_COPY_NT,
+ KNOB_LIGHT_BYTES) = range(1, 8)
 
 
 def debug_get(knob: int) -> int:

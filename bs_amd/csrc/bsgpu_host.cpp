@@ -275,6 +275,7 @@ std::atomic<int64_t>& knob(int k) {
     const char* e = std::getenv("BSG_COPY_NT");
     return e ? (int64_t)(std::strtoull(e, nullptr, 10) != 0) : (int64_t)1;
   }()};
+  static std::atomic<int64_t> light_bytes{(int64_t)(4ull << 30)};  // engine runs: light schedule
   static std::atomic<int64_t> none{0};
   switch (k) {
     case BSG_KNOB_SEQ_WAIT: return seq_wait;
@@ -283,6 +284,7 @@ std::atomic<int64_t>& knob(int k) {
     case BSG_KNOB_EARLY: return early;
     case BSG_KNOB_POLL: return poll;
     case BSG_KNOB_COPY_NT: return copy_nt;
+    case BSG_KNOB_LIGHT_BYTES: return light_bytes;
     default: return none;
   }
 }
@@ -379,13 +381,13 @@ struct bsg_engine {
     return !snapshot && !hash_mode && knob(BSG_KNOB_EARLY) != 0;
   }
 
-  // Round 5: a lightly loaded run (at most kLightBytes, where the longest chunk's chain is the
-  // step: configs[1], [3], [4]) keeps its early chains on the engine stream right after k_pick
-  // and moves selection and k_sha to the second stream, so the chain pays no cross-stream wait
-  // (≈ 10-14 us between k_compact and k_pick, profiles/r04_run_timelines_early.txt) and no
-  // dispatch gap; selection, which has slack there, pays it instead. A loaded run (configs[2],
-  // where the hash work ends with the chain) keeps selection on the engine stream.
-  static constexpr uint64_t kLightBytes = 4ull << 30;
+  // Round 5: a lightly loaded run (at most BSG_KNOB_LIGHT_BYTES, default 4 GiB, where the
+  // longest chunk's chain is the step: configs[1], [3], [4]) keeps its early chains on the
+  // engine stream right after k_pick and moves selection and k_sha to the second stream, so the
+  // chain pays no cross-stream wait (≈ 10-14 us between k_compact and k_pick,
+  // profiles/r04_run_timelines_early.txt) and no dispatch gap; selection, which has slack there,
+  // pays it instead. A loaded run (configs[2], where the hash work ends with the chain) keeps
+  // selection on the engine stream. The knob lets the tests run one input both ways.
 
   // profile 1: every stage boundary; 2: the SHA-256 stage's two only (on the stream it runs on)
   void mark(int i, hipStream_t on = nullptr) {
@@ -534,7 +536,7 @@ struct bsg_engine {
     if (strips) HCHECK(dbg("launch_compact", stream, launch_compact(sa, stream, num_cus)));
     // (exits at once unless a strip had more candidates than slots; k_pick needs them all)
     if (strips) HCHECK(dbg("launch_rescan", stream, launch_rescan(sa, stream, num_cus)));
-    const bool light = early && total_len <= kLightBytes;
+    const bool light = early && total_len <= (uint64_t)knob(BSG_KNOB_LIGHT_BYTES).load();
     hipStream_t sel_stream = stream;  // where selection and k_sha run
     if (early && light) {  // chains on the engine stream, selection beside them
       HCHECK(dbg("launch_pick", stream,
@@ -2474,6 +2476,20 @@ struct bsg_hasher {
   }
 
   int sum(const uint8_t* base, const uint64_t* o, const uint64_t* l, uint32_t n, uint8_t* out) {
+    static const bool dbg_times = std::getenv("BSG_DEBUG_HASHER") != nullptr;
+    const auto t_in = std::chrono::steady_clock::now();
+    struct Report {  // BSG_DEBUG_HASHER: where one call's time went (stderr)
+      bool on;
+      std::chrono::steady_clock::time_point t0;
+      uint32_t n;
+      uint64_t marks[4] = {};
+      ~Report() {
+        if (on)
+          std::fprintf(stderr, "bsgpu hasher: %u blobs, %.3f ms (ensure %.3f, copies %.3f, launch %.3f)\n",
+                       n, ns_since(t0) / 1e6, marks[0] / 1e6, (marks[1] - marks[0]) / 1e6,
+                       (marks[2] - marks[1]) / 1e6);
+      }
+    } rep{dbg_times, t_in, n};
     hipPointerAttribute_t attr;
     bool on_device = false;
     if (hipPointerGetAttributes(&attr, base) == hipSuccess)
@@ -2503,6 +2519,7 @@ struct bsg_hasher {
     // and would stay held for the life of the process).
     const bool via_pinned = !on_device && hi <= kEngineMinBytes;
     HCHECK(h_small.ensure(std::max<uint64_t>(via_pinned ? hi : 0, 32ull * n)));
+    rep.marks[0] = ns_since(t_in);
     if (hi) {
       if (on_device) {
         HCHECK(hipMemcpyAsync(data.p, base, hi, hipMemcpyDeviceToDevice, stream));
@@ -2516,9 +2533,11 @@ struct bsg_hasher {
     HCHECK(hipMemcpyAsync(off.p, h_meta.p, 8ull * n, hipMemcpyHostToDevice, stream));
     HCHECK(hipMemcpyAsync(len.p, h_meta.as<uint8_t>() + 8ull * n, 8ull * n,
                           hipMemcpyHostToDevice, stream));
+    rep.marks[1] = ns_since(t_in);
     BlobShaArgs a{data.as<uint8_t>(), off.as<uint64_t>(), len.as<uint64_t>(), n,
                   refs.as<uint8_t>()};
     HCHECK(launch_sha_blobs(a, stream, num_cus));
+    rep.marks[2] = ns_since(t_in);
     HCHECK(hipMemcpyAsync(h_small.p, refs.p, 32ull * n, hipMemcpyDeviceToHost, stream));
     HCHECK(hipStreamSynchronize(stream));
     std::memcpy(out, h_small.p, 32ull * n);

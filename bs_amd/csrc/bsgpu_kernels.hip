@@ -1112,12 +1112,16 @@ __device__ __forceinline__ void lane_words(const ShaJob& jb, uint32_t blk, const
   }
 }
 
-// A region's pop counter: the jobs taken from it so far (longest first); the jobs left are
-// rorder[off + hd .. off + n). Returns hd, or n when no job is left.
+// A region's pop counter: the jobs taken from it so far (longest first) in its low word, a
+// region holding fewer than 2^32 jobs; the high word stays zero (round 5 counted jobs taken from
+// the region's tail there, for an experiment since dropped), and is kept in the test below and in
+// sha_lane_mode's pop: without it the per-lane loop compiled to a different layout and ran 3 %
+// slower per block (6,400-6,500 against 6,290 cycles, profiles/r06_c3_c2_*.log).
+// Returns hd, or n when no job is left (the jobs left are rorder[off + hd .. off + n)).
 __device__ __forceinline__ uint64_t reg_head(const ShaArgs& a, uint32_t r, uint64_t n) {
-  const uint64_t hd =
-      __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return hd < n ? hd : n;
+  const uint64_t v = __hip_atomic_load(&a.reg->head[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t hd = (uint32_t)v, hi = v >> 32;
+  return hd + hi < n ? hd : n;
 }
 
 // The region whose next job is the longest (longest-first across regions, so the last jobs
@@ -1288,10 +1292,11 @@ __device__ void sha_lane_mode(const ShaArgs& a, uint64_t M) {
       nj_d = nj;  // its descriptor is loaded below
       stage = 5;
     } else if (stage == 1) {
-      // the region's pop count before this pop (a region holds < 2^32 jobs)
+      // the region's pop count before this pop (reg_head: low word; the high word is zero)
       const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pop_base, pop_leader);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pop_base >> 32), pop_leader);
       const uint64_t local = (uint64_t)lo + pop_rank;
-      dry = local >= pop_n;
+      dry = local + hi >= pop_n;
       q = pop_off + local;
       stage = dry ? 0u : 2u;  // its job id is loaded below; else the region ran dry
     }
@@ -2034,7 +2039,7 @@ __device__ __forceinline__ bool solo_chain_blocks(const ShaArgs& a, uint32_t nb,
     if (!lds_seq_wait(a, fill_seq + h, f / 2 + 1)) return false;
     const uint32_t* krow = ol.a_side ? ones : lds + (2 * c + h) * kHelpHalfWords;
     const uint32_t stride = ol.a_side ? 0u : 4u * kLongRow;
-    sha256_blocks_oct(hs, krow, stride, min(64u, nb - base), (int32_t)nb - (int32_t)base, ol);
+    sha256_blocks_oct_solo(hs, krow, stride, min(64u, nb - base), ol);
     if (lane == 0) lds_seq_store(done_seq + h, f / 2 + 1);
   }
   // H0..H3 from octet position 4 (an A lane), H4..H7 from position 0 (an E lane)
@@ -2227,6 +2232,13 @@ __global__ __launch_bounds__(kShaBlock, 1) void k_sha(ShaArgs a) {
 // a sync point (E_i - E_i-1 >= MinSize: k_select makes it a boundary whatever came before) and
 // c_i+1 is one too or is the forced final flush. Chunks below the wave-mode floor are not worth
 // the second stream. Keys are (blocks << 32 | i), so all keys differ.
+// Such a chunk always satisfies k_lens's match (fin, prefix == 0, consumed == 0): it starts at
+// the boundary c_i, after c_i-1 of the same segment, so it is never a segment's first chunk —
+// the only one that can hold head bytes or a midstate carried in (prefix, consumed) — and it
+// ends at a boundary, so it is never the open chunk a non-final segment leaves (fin). A pick
+// that k_lens still does not match is a selection bug, flagged by k_early_fix (device error 16).
+// (Engine runs start every stream fresh, open_start == seg_base == 0; streaming engines, whose
+// segments carry open chunks, never run early chains: early_ok() requires !snapshot.)
 __device__ __forceinline__ uint64_t pick_key(const uint64_t* __restrict__ cand, uint64_t n,
                                              uint64_t i, uint64_t minsz) {
   if (i == 0 || i + 1 >= n) return 0;

@@ -444,4 +444,26 @@ __device__ __forceinline__ void sha256_blocks_oct(uint32_t (&hs)[4], const uint3
                : "memory", BSG_OCT_LOOP_CLOBBERS);
 }
 
+// The same loop for a chain that runs alone in its wave (every octet the same chain: solo
+// tickets, helped solo chains, k_early): no per-block exec update, no slot copies, K+W quads
+// read eight at a time and no s_nop (tools/gen_skew_asm.py, main_loop_oct_solo): 560
+// instructions per block against 570.
+#include "sha256_oct_solo_loop.inc"
+__device__ __forceinline__ void sha256_blocks_oct_solo(uint32_t (&hs)[4], const uint32_t* row,
+                                                       uint32_t stride, uint32_t nblk,
+                                                       const OctLane& b) {
+  if (nblk == 0) return;
+  nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)nblk);  // (see sha256_blocks_oct)
+  const uint32_t addr = (uint32_t)reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const uint32_t*)row);
+  const uint64_t amask = 0xF0F0F0F0F0F0F0F0ull;  // A lanes: octet positions 4-7
+  uint32_t cnt;
+  asm volatile(BSG_OCT_SOLO_LOOP_ASM
+               : [h0] "+v"(hs[0]), [h1] "+v"(hs[1]), [h2] "+v"(hs[2]), [h3] "+v"(hs[3]),
+                 [cnt] "=&s"(cnt)
+               : [addr] "v"(addr), [stride] "v"(stride), [nblk] "s"(nblk), [xm] "v"(b.xm),
+                 [s1] "v"(b.rot), [amask] "s"(amask)
+               : "memory", BSG_OCT_SOLO_LOOP_CLOBBERS);
+}
+
 }  // namespace bsg

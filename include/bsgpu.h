@@ -335,7 +335,11 @@ void bsg_reader_free(bsg_reader* r);
 #define BSG_KNOB_COPY_NT 6       /* BSG_COPY_NT: 1 (default) copies Write bytes into pinned
                                   * staging (and the Writer's pieces) with non-temporal stores;
                                   * 0 uses memcpy */
-#define BSG_KNOB_LAST BSG_KNOB_COPY_NT
+#define BSG_KNOB_LIGHT_BYTES 7  /* engine runs of at most this many bytes (default 4 GiB) keep
+                                  * their early chains on the engine stream and move selection
+                                  * and k_sha to the second stream; larger runs the other way
+                                  * (tests run one input both ways) */
+#define BSG_KNOB_LAST BSG_KNOB_LIGHT_BYTES
 int bsg_debug_set(int knob, int64_t value);
 int64_t bsg_debug_get(int knob); /* -1 for an unknown knob */
 

@@ -1,5 +1,6 @@
 """C-ABI library: builds, loads, exports every symbol include/bsgpu.h declares (no GPU needed)."""
 import ctypes
+import os
 import subprocess
 
 import numpy as np
@@ -81,7 +82,7 @@ def test_debug_knobs_and_null_handles():
     from bs_amd import bsgpu
     L = bsgpu.lib()
     for knob in (bsgpu.KNOB_SEQ_WAIT, bsgpu.KNOB_LONG_MODE, bsgpu.KNOB_VERIFY_WINDOW,
-                 bsgpu.KNOB_EARLY, bsgpu.KNOB_POLL):
+                 bsgpu.KNOB_EARLY, bsgpu.KNOB_POLL, bsgpu.KNOB_COPY_NT, bsgpu.KNOB_LIGHT_BYTES):
         old = bsgpu.debug_get(knob)
         assert old >= 0
         with bsgpu.debug_knob(knob, 1):
@@ -91,6 +92,12 @@ def test_debug_knobs_and_null_handles():
     assert L.bsg_debug_set(bsgpu.KNOB_SEQ_WAIT, -1) == -22
     assert L.bsg_debug_set(bsgpu.KNOB_EARLY, 2) == -22       # 0 off, 1 on
     assert L.bsg_debug_set(bsgpu.KNOB_POLL, 2) == -22        # 0 block, 1 poll
+    assert L.bsg_debug_set(bsgpu.KNOB_COPY_NT, 2) == -22     # 0 memcpy, 1 non-temporal
+    if "BSG_POLL" not in os.environ:
+        assert bsgpu.debug_get(bsgpu.KNOB_POLL) == 1         # the bounded poll is the default
+    if "BSG_COPY_NT" not in os.environ:
+        assert bsgpu.debug_get(bsgpu.KNOB_COPY_NT) == 1
+    assert bsgpu.debug_get(bsgpu.KNOB_LIGHT_BYTES) == 4 << 30
     assert L.bsg_debug_set(99, 0) == -22 and L.bsg_debug_get(99) == -1
     out = np.zeros(4, dtype=np.uint64)
     assert L.bsg_reader_stats(None, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) == -22

@@ -369,6 +369,38 @@ def test_early_chains_on_off(gpu, oracle, table):
     assert tl0 and tl0["long_start"] >= 0, got[0][2]
 
 
+def test_early_chains_light_and_loaded_schedules(gpu, oracle, table):
+    """every test input is at most the 4 GiB light-run threshold, so the loaded
+    schedule (selection and k_sha on the engine stream, k_pick on the second one, k_lens waiting
+    for the pick) ran only in the bench's configs[2] leg. BSG_KNOB_LIGHT_BYTES moves the
+    threshold: the same 300 MiB batch with the early chains runs both ways, and both give the
+    oracle's records."""
+    from bs_amd.synth import splitmix_array
+    lens = [190 << 20, (110 << 20) + 12345]
+    seeds = [0x5EED1, 0x5EED2]
+    want = [oracle.split(table, splitmix_array(s, n)) for s, n in zip(seeds, lens)]
+    stride = [(n + 15) & ~15 for n in lens]
+    buf = gpu.DeviceBuffer(sum(stride) + 4096)
+    offs = [0, stride[0]]
+    for o, n, s in zip(offs, lens, seeds):
+        gpu.fill_splitmix(buf.ptr + o, n, s)
+    gpu.synchronize()
+    got = {}
+    for light in (4 << 30, 0):
+        with gpu.debug_knob(gpu.KNOB_LIGHT_BYTES, light), gpu.debug_knob(gpu.KNOB_EARLY, 1):
+            eng = gpu.Engine()
+            eng.run(buf.ptr, offs, lens)
+            eng.finish()
+            got[light] = (as_tuples(eng.chunks()), [int(c) for c in eng.counts()], eng.diag())
+            eng.close()
+    buf.free()
+    for light, (ch, counts, diag) in got.items():
+        assert counts == [len(w) for w in want], light
+        assert ch == as_tuples(want[0]) + as_tuples(want[1]), light
+    tl = got[4 << 30][2].get("timeline_us")
+    assert tl and tl["long_start"] < 0, got[4 << 30][2]  # light: the longest chain ran early
+
+
 @pytest.mark.parametrize("bits,min_size", [(13, 8192), (20, 64), (16, 65536), (14, 1)])
 def test_early_chains_params(gpu, oracle, table, bits, min_size):
     """The sure-boundary rule behind the early picks (E_i - E_i-1 >= MinSize) under other

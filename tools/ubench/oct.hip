@@ -50,7 +50,10 @@ __global__ __launch_bounds__(64) void kb(uint64_t* out, uint32_t* io, int blocks
     uint32_t hs[4];
     for (int k = 0; k < 4; ++k) hs[k] = ol.a_side ? st[k] : st[emap[k]];
     STAMP(t0);
-    sha256_blocks_oct(hs, rows[ol.a_side ? 1 : 0], 0u, (uint32_t)blocks, blocks, ol);
+    if (V == 3)  // the solo loop (round 6): no exec update, no slot copies, no s_nop
+      sha256_blocks_oct_solo(hs, rows[ol.a_side ? 1 : 0], 0u, (uint32_t)blocks, ol);
+    else
+      sha256_blocks_oct(hs, rows[ol.a_side ? 1 : 0], 0u, (uint32_t)blocks, blocks, ol);
     STAMP(t1);
     if (threadIdx.x == 0 || threadIdx.x == 4)
       for (int k = 0; k < 4; ++k) io[2000 + (threadIdx.x == 4 ? k : emap[k])] = hs[k];
@@ -73,7 +76,7 @@ template <int V> bool run(const char* name, uint32_t* ref, int blocks) {
   bool ok = true;
   if (V == 0) for (int i = 0; i < 8; ++i) ref[i] = fin[i];
   else for (int i = 0; i < 8; ++i) ok &= ref[i] == fin[i];
-  if (V == 2) {
+  if (V >= 2) {
     uint32_t all[256]; (void)hipMemcpy(all, io + 3000, 1024, hipMemcpyDeviceToHost);
     for (int l = 0; l < 64; ++l)
       for (int k = 0; k < 4; ++k) ok &= all[4 * l + k] == all[4 * (l & 4) + k];
@@ -92,6 +95,7 @@ int main() {
     run<0>("single lane (14 VALU/round)", ref, blocks);
     ok &= run<1>("skewed pair loop (9 VALU/round)", ref, blocks);
     ok &= run<2>("skewed octet loop (8 VALU/round)", ref, blocks);
+    ok &= run<3>("skewed octet solo loop (round 6)", ref, blocks);
   }
   return ok ? 0 : 1;
 }

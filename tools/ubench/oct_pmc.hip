@@ -12,5 +12,10 @@ int main() {
   if (hipDeviceSynchronize() != hipSuccess) return 1;
   uint64_t h; (void)hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
   printf("octet chain, 4000 blocks: %.1f cycles/block\n", (double)h / 4000);
+  // round 6: the solo loop (sha256_blocks_oct_solo), same launches
+  for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(kb<3>, dim3(1), dim3(64), 0, 0, d, io, 4000);
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  (void)hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+  printf("octet solo chain, 4000 blocks: %.1f cycles/block\n", (double)h / 4000);
   return 0;
 }
