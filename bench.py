@@ -623,7 +623,13 @@ def main():
 
     build_once(world, local)
     assert bsgpu.device_count() > local, "bench.py needs a GPU (the HIP path is the product)"
-    if os.environ.get("BSG_BENCH_INIT") == "1":  # bsg_init up front, as a server does (A/B)
+    # bsg_init up front, as a server does at start-up (include/bsgpu.h): the device, the pooled
+    # streams and the pinned stage ring are set up before the legs' own large host allocations.
+    # Without it the host-memory legs varied from rep to rep (the final tile 8.3-12.8 ms, the
+    # Writer's copies 24 against 17 ms per GiB; profiles/r06_c4_legs_*.log). BSG_BENCH_INIT=0
+    # skips it (A/B).
+    init = os.environ.get("BSG_BENCH_INIT", "1") != "0"
+    if init:
         bsgpu.init(local)
     nbytes = args.stream_mib << 20
     ns = args.streams
@@ -664,10 +670,12 @@ def main():
                                     min_size=args.min_size, fanout=8)
         del data
         wr["root_check"] = wr["root"] == ref_root.hex()
+        wr["bsg_init"] = init
     if e2e is not None:
         # the e2e stream is the same SplitMix64 stream as configs[1]'s (seed BASE_SEED): when the
         # device leg's oracle split covered that whole stream, the host-path records are checked
         # against it too (bsg_write -> records in host memory, bit for bit)
+        e2e["bsg_init"] = init
         recs, ref = e2e.pop("records"), leg.get("ref")
         if ref is not None and e2e["bytes"] == nbytes:
             e2e["oracle_check"] = records_match(recs, None, ref, 1, True)

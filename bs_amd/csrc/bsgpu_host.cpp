@@ -364,6 +364,7 @@ struct bsg_engine {
   uint32_t nstreams = 0;
   bool enqueued = false;
   bool hash_mode = false;  // bsg_engine_hash: every stream is one blob (enqueue_hash)
+  int hash_long_mode = -1;  // >= 0: enqueue_hash's SHA path choice instead of the knob's
   Counters last{};
   // optional per-stage HIP events on the engine stream: [scan, compact..chunks, sha]
   int profile = 0;  // bsg_engine_profile mode
@@ -658,7 +659,8 @@ struct bsg_engine {
                buckets.as<uint32_t>() + 2 * kLptBuckets, buckets.as<uint32_t>() + 3 * kLptBuckets,
                jinfo.as<uint32_t>(), jdesc.as<LaneJob>(), regions.as<Regions>(), oreg.as<uint8_t>(),
                data_span > kRegionBytes ? rorder.as<uint64_t>() : order.as<uint64_t>(), data_span,
-               long_mode(), 4u * (uint32_t)num_cus, seq_wait_limit()};
+               hash_long_mode >= 0 ? hash_long_mode : long_mode(), 4u * (uint32_t)num_cus,
+               seq_wait_limit()};
     HCHECK(dbg("launch_longlist", stream, launch_longlist(sh, chunk_cap + ns, stream, num_cus)));
     mark(2);
     HCHECK(dbg("launch_sha", stream, launch_sha(sh, chunk_cap + ns, stream, num_cus)));
@@ -2404,6 +2406,7 @@ struct bsg_hasher {
   // so a batch waits for its longest blob at per-lane speed, ~2.5x slower per block).
   static constexpr uint32_t kEngineMinBlobs = 16;
   static constexpr uint64_t kEngineMinBytes = 4ull << 20;
+  static constexpr uint64_t kEngineLongBlob = 16ull << 10;  // (small batches, see sum())
   static constexpr uint64_t kEngineBatch = 256ull << 20;  // bytes per engine run (one blob may exceed)
   static constexpr uint64_t kGatherPiece = 32ull << 20;   // packed and copied to the device at once
   bsg_engine* eng = nullptr;
@@ -2421,6 +2424,9 @@ struct bsg_hasher {
     stage.dma_only = true;  // read only by the H2D: a registered huge-page mapping pins faster
     uint64_t left = 0;      // bytes of the blobs not yet in a run
     for (uint32_t k = 0; k < n; ++k) left += l[k];
+    // a small batch (see sum()) puts every blob on wave tickets: the engine's own choice keeps
+    // blobs under kLongMinBlocks (64 KiB) per-lane
+    eng->hash_long_mode = left < kEngineMinBytes ? 2 : -1;
     for (uint32_t i = 0; i < n;) {
       // A run is up to kEngineBatch bytes, or everything left if that is at most a quarter more:
       // every run waits for its longest blob's chain (~10 ms for a 256 MiB run), so a small
@@ -2496,12 +2502,21 @@ struct bsg_hasher {
       on_device = (attr.type == hipMemoryTypeDevice);
     else
       (void)hipGetLastError();
-    uint64_t hi = 0, total = 0;
+    uint64_t hi = 0, total = 0, longest = 0;
     for (uint32_t i = 0; i < n; ++i) {
       hi = std::max<uint64_t>(hi, o[i] + l[i]);
       total += l[i];
+      longest = std::max<uint64_t>(longest, l[i]);
     }
     if (!on_device && n >= kEngineMinBlobs && total >= kEngineMinBytes)
+      return sum_engine(base, o, nullptr, l, n, out);
+    // A small batch with a long blob goes to the engine too, every blob on a wave ticket: one
+    // blob per lane hashes a block per ~6,000-8,000 cycles and the batch waits for its longest
+    // blob, where a solo wave chain takes ~2,300 (plus ~0.1 ms of launches). A split::Writer's tree nodes are such a batch:
+    // their leaf counts are geometric, so 1 GiB's 63 nodes of ~11 KB include one of ~50 KB, and
+    // k_sha_blobs took 2.7-3.1 ms for them (profiles/r06_writer_trace_kernel_stats.csv). Its
+    // staging stays the batch's size (< kEngineMinBytes), so a pooled hasher pins nothing big.
+    if (!on_device && n >= 2 && total < kEngineMinBytes && longest >= kEngineLongBlob)
       return sum_engine(base, o, nullptr, l, n, out);
     // always hash from a private copy with kReadSlack bytes of tail padding
     HCHECK(data.ensure(hi + kReadSlack));

@@ -97,6 +97,27 @@ def test_hasher_large_blob_small_path_pins_nothing_big(gpu):
         h.free()
 
 
+@pytest.mark.parametrize("long_kib", [15, 16, 50, 900])
+def test_hasher_small_batch_with_a_long_blob(gpu, long_kib):
+    """Round 6: a batch under the engine's byte threshold that holds a blob of 16 KiB or more
+    (a split::Writer's tree nodes: geometric leaf counts) goes to the engine's wave-mode chains
+    instead of one blob per lane; at 15 KiB it stays on the per-lane path. Both forms, through
+    bsg_hasher_sum and _sum_ptrs, against hashlib; the hasher pins only the batch's size."""
+    rng = np.random.default_rng(long_kib)
+    blobs = [rng.bytes(int(n)) for n in rng.integers(0, 12_000, 62)]
+    blobs.insert(17, rng.bytes(long_kib << 10))
+    blobs.insert(3, b"")
+    want = [hashlib.sha256(b).digest() for b in blobs]
+    h = gpu.Hasher()
+    try:
+        assert h.sum(blobs) == want
+        assert h.sum_ptrs(blobs) == want
+        assert h.sum(blobs[:2]) == want[:2]
+        assert h.pinned_bytes() < 8 << 20, h.pinned_bytes()
+    finally:
+        h.free()
+
+
 def test_sha256_batch_over_65535_blobs(gpu):
     rng = np.random.default_rng(8)
     lens = rng.integers(0, 160, 70_000)
