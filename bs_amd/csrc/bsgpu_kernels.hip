@@ -19,6 +19,7 @@
 #include "bsgpu_internal.h"
 #include "bsgpu_launch.h"
 #include "sha256_device.h"
+#include "scan_block_loop.inc"
 
 // Wave-mode rounds run split over lanes: skewed pairs (9 VALU per round, 2,941 cycles per
 // block on MI355X) and skewed octets (8 VALU, 2,330 at round 5); one lane running the whole
@@ -210,46 +211,26 @@ __device__ __forceinline__ bool table_at_lds0(const uint32_t* tab) {
   return (uint32_t)(uintptr_t)((lds_u32p)tab) == 0u;
 }
 
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-
-// One 64-byte block of the fast loop, software-pipelined: hin[] holds the table values of the
-// previous block (the out-going bytes), hcur[] those of this block (looked up one block
+// One 64-byte block of the compiled fast loop (the narrow pre-filter, split_bits < 16; the
+// WIDE form is the asm statement of scan_span), software-pipelined: hin[] holds the table values
+// of the previous block (the out-going bytes), hcur[] those of this block (looked up one block
 // earlier). As soon as step k has consumed hin[k], the lookup of byte k of the NEXT block is
 // issued into that register, so ~64 LDS reads are in flight behind the hash chain instead of
 // sitting in front of it, and the two arrays swap roles every block (no register moves).
-// Candidate pre-filter per block:
-//   WIDE (split_bits >= 16): packed min of the low 16 bits of two hashes (v_perm + v_pk_min_u16);
-//   else: min3 of (h & mask).
-// Any block whose pre-filter hits is re-scanned exactly by slow_block().
-template <bool WIDE, bool LOAD>
+// Candidate pre-filter per block: min3 of (h & mask); a block whose pre-filter hits is re-scanned
+// exactly by k_scan's exact pass.
+template <bool LOAD>
 __device__ __forceinline__ bool chain64(const uint32_t* tab, const uint32_t (&wnext)[16],
                                         uint32_t (&hin)[64], const uint32_t (&hcur)[64],
                                         uint32_t& h, uint32_t lane4, uint32_t mask) {
-  if (WIDE) {
-    // min of the low 16 bits of the running min and both hashes in one v_min3_u16 (round 1:
-    // a v_perm packing two hashes + a v_pk_min_u16, one VALU per byte instead of a half)
-    uint32_t m = 0xffffu;
+  uint32_t m = 0xffffffffu;
 #pragma unroll
-    for (int k = 0; k < 64; k += 2) {
-      const uint32_t h0 = xor3(rotl1(h), hin[k], hcur[k]);
-      h = xor3(rotl1(h0), hin[k + 1], hcur[k + 1]);
-      if (LOAD) {
-        hin[k] = lds_at(tab, tab_addr(wnext[k >> 2], lane4, k));
-        hin[k + 1] = lds_at(tab, tab_addr(wnext[(k + 1) >> 2], lane4, k + 1));
-      }
-      asm("v_min3_u16 %0, %1, %2, %3" : "=v"(m) : "v"(m), "v"(h0), "v"(h));
-    }
-    return (m & 0xffffu) == 0;
-  } else {
-    uint32_t m = 0xffffffffu;
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-      h = xor3(rotl1(h), hin[k], hcur[k]);
-      if (LOAD) hin[k] = lds_at(tab, tab_addr(wnext[k >> 2], lane4, k));
-      m = min(m, h & mask);
-    }
-    return m == 0;
+  for (int k = 0; k < 64; ++k) {
+    h = xor3(rotl1(h), hin[k], hcur[k]);
+    if (LOAD) hin[k] = lds_at(tab, tab_addr(wnext[k >> 2], lane4, k));
+    m = min(m, h & mask);
   }
+  return m == 0;
 }
 
 __device__ __forceinline__ void lookup64(const uint32_t* tab, const uint32_t (&w)[16],
@@ -265,7 +246,6 @@ __device__ __forceinline__ void lookup64(const uint32_t* tab, const uint32_t (&w
 // nothing but the two histories, two word blocks and the hash (no call, no scratch).
 static_assert(kStrip / 64 <= 32, "one 32-bit hit mask per strip (kStrip <= 2 KiB)");
 
-template <bool WIDE>
 __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const uint32_t* tab,
                                                      uint32_t lane4, const uint8_t* base,
                                                      uint32_t nfull, uint32_t& h,
@@ -284,9 +264,9 @@ __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const ui
     load16(base + 64ull * min(b + 2, nfull - 1), n0);  // the next line (clamped, branch-free)
     load16(base + 64ull * min(b + 3, nfull - 1), n1);
     // block b: out-going hA, in-coming hB; looks up block b+1 into hA
-    hits |= chain64<WIDE, true>(tab, w1, hA, hB, h, lane4, mask) ? 1u << b : 0u;
+    hits |= chain64<true>(tab, w1, hA, hB, h, lane4, mask) ? 1u << b : 0u;
     // block b+1: out-going hB, in-coming hA; looks up block b+2 into hB
-    hits |= chain64<WIDE, true>(tab, n0, hB, hA, h, lane4, mask) ? 1u << (b + 1) : 0u;
+    hits |= chain64<true>(tab, n0, hB, hA, h, lane4, mask) ? 1u << (b + 1) : 0u;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       w0[i] = n0[i];
@@ -294,7 +274,7 @@ __device__ __forceinline__ uint32_t scan_full_blocks(const ScanArgs& a, const ui
     }
   }
   if (b < nfull) {  // odd block count: the last block, then its values back into hA
-    hits |= chain64<WIDE, false>(tab, w1, hA, hB, h, lane4, mask) ? 1u << b : 0u;
+    hits |= chain64<false>(tab, w1, hA, hB, h, lane4, mask) ? 1u << b : 0u;
 #pragma unroll
     for (int k = 0; k < 64; ++k) hA[k] = hB[k];
   }
@@ -371,29 +351,46 @@ __device__ __forceinline__ StripJob strip_job(const ScanArgs& a, uint64_t strip,
 // hit bit per block whose pre-filter fires. The strip's first line is loaded with its history
 // block (one HBM round trip per strip start instead of two; a short strip reads within
 // kReadSlack), then the window is warmed on the history in the running form h = rotl1(h) ^ t.
+// WIDE (split_bits >= 16, every default run): one generated asm statement
+// (tools/gen_scan_loop.py, scan_block_loop.inc) with every 8-byte instruction 8-byte aligned,
+// 324 instructions per block against hipcc's 390 (536 of its 1,559 per four blocks started at
+// 4 mod 8): configs[2]'s k_scan 3.49-3.55 -> 3.22-3.30 ms (round 6,
+// profiles/r06_c8_*). The narrow pre-filter keeps the compiled loop (scan_full_blocks).
 // (Round 5 measured and dropped: the warm-up as independent rotates folded by xor3, and chained
 // strips — lane l continuing lane l-1's strip so that the history block is not read again —
 // which cut k_scan's reads from 1.069x to 1.007x of its input but ran 4-7 % longer,
 // profiles/r05_ab20_*.log: the loop is not bound by HBM bytes alone.)
 template <bool WIDE>
 __device__ __forceinline__ uint32_t scan_span(const ScanArgs& a, const uint32_t* tab,
-                                              uint32_t lane4, const StripJob& j, uint32_t& h,
-                                              uint32_t (&hist)[64]) {
+                                              uint32_t lane4, const StripJob& j) {
   const uint32_t nfull = j.len >> 6;
   const uint8_t* base = j.d + j.start;
-  uint32_t w[16], w0[16], w1[16];
+  if (WIDE) {
+    // operands: the LDS address selectors of tab_addr() for bytes 0-3 of a word; the statement
+    // owns v40-v247 (histories, two line buffers, hash, addresses) and restores exec
+    uint32_t hits, b, sb;
+    uint64_t sexec;
+    asm volatile(BSG_SCAN_LOOP_ASM
+                 : [hits] "=v"(hits), [sexec] "=&s"(sexec), [b] "=&s"(b), [sb] "=&s"(sb)
+                 : [nfull] "v"(nfull), [lane4] "v"(lane4), [pre] "v"(j.pre), [base] "v"(base),
+                   [sel0] "s"(0x0c0c0400u), [sel1] "s"(0x0c0c0500u), [sel2] "s"(0x0c0c0600u),
+                   [sel3] "s"(0x0c0c0700u)
+                 : BSG_SCAN_LOOP_CLOBBERS);
+    return hits;
+  }
+  uint32_t w[16], w0[16], w1[16], hist[64];
   load16(j.pre, w);
   load16(base, w0);
   load16(base + 64ull * min(1u, nfull - 1), w1);
   __builtin_amdgcn_sched_barrier(0);
-  h = 0;
+  uint32_t h = 0;
 #pragma unroll
   for (int k = 0; k < 64; ++k) {
     uint32_t t = lds_at(tab, tab_addr(w[k >> 2], lane4, k));
     h = rotl1(h) ^ t;
     hist[k] = t;
   }
-  return nfull ? scan_full_blocks<WIDE>(a, tab, lane4, base, nfull, h, hist, w0, w1) : 0u;
+  return nfull ? scan_full_blocks(a, tab, lane4, base, nfull, h, hist, w0, w1) : 0u;
 }
 
 // Appends the flagged strips of a wave to its workgroup's refine list (refine + blockIdx.x *
@@ -531,9 +528,8 @@ __global__ __launch_bounds__(kScanThreads, 2) void k_scan(ScanArgs a) {
     bool flag = false;
     uint32_t hits = 0;
     const bool in = strip < a.nstrips;
-    uint32_t hist[64], h = 0;
     if (in) {
-      hits = scan_span<WIDE>(a, tab, lane4, cur, h, hist);
+      hits = scan_span<WIDE>(a, tab, lane4, cur);
       a.counts[strip] = 0u;
       flag = hits || cur.tail;
     }

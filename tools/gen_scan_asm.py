@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""EXPERIMENT, NOT IN THE BUILD: k_scan's rolling buzhash32 over all full
+"""ROUNDS 1-2 EXPERIMENT, NOT IN THE BUILD; the product form since round 6 is
+tools/gen_scan_loop.py (the same loop with every 8-byte instruction aligned). Here: k_scan's rolling buzhash32 over all full
 64-byte blocks of one lane's strip (split_bits >= 16 pre-filter) as ONE inline-asm statement.
 It was wired in as `scan_blocks_asm(pre, base, nfull, lane4, h, hits)` (outputs: the hash after
 the last full block and one bit per pre-filter hit; a k_scan<ASM> template so the compiled loop
@@ -34,7 +35,7 @@ landed whenever at most 15 are outstanding.
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "bs_amd", "csrc", "scan_block_loop.inc")
+OUT = os.path.join(ROOT, "bs_amd", "variants", "scan_block_loop_r01.inc")  # not the product include
 
 # fixed registers (the compiler keeps everything else in v0-v71 and v244-v255)
 H, H0, M, PK, A0, A1, T = (f"v{72 + i}" for i in range(7))   # v79: JUNK
