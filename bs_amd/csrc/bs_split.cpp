@@ -758,10 +758,10 @@ Status Writer::Copy(const uint8_t* p, size_t n, uint8_t* dst) {
     const size_t nt = std::min<size_t>((size_t)bsg::copy_threads(), k / kPerThread);
     if (nt <= 1) {
       work(0, k);
-    } else {
-      const size_t per = ((k + nt - 1) / nt + 4095) & ~(size_t)4095;
-      bsg::parallel_for((k + per - 1) / per,
-                        [&](size_t t) { work(t * per, std::min(k, t * per + per)); });
+    } else {  // kCopySlice slices taken dynamically (a late or slow thread takes fewer)
+      constexpr size_t sl = bsg::kCopySlice;
+      bsg::parallel_for((k + sl - 1) / sl,
+                        [&](size_t t) { work(t * sl, std::min(k, t * sl + sl)); });
     }
     rc = bsg_write_commit(ctx_, k);
     if (rc) return Status::Err(rc, std::string("bsg_write_commit: ") + bsg_errstr(rc));

@@ -40,6 +40,8 @@
 
 using namespace bsg;
 
+int device_node(int device);  // NUMA node of a HIP device (below)
+
 namespace {
 
 const uint32_t kIV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
@@ -102,6 +104,23 @@ static inline void tsan_after_alloc() {}
 static inline void tsan_before_free() {}
 #endif
 
+// DMA staging pages on the current device's NUMA node (preferred, not bound: a full node falls
+// back to the other). The H2D of a stage on the far node ran at 49.4-49.7 GB/s against
+// 56.2-56.3 from the GPU's own node, the same box and library (profiles/r06_c6_bench1.log /
+// bench2.log, bsg_stream_stats), so the 1 GiB e2e took 31.0 ms a rep instead of 28.3: the pages
+// were simply placed by first touch, on whichever node the registering thread ran.
+void prefer_device_node(void* m, size_t n) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  const int node = device_node(dev);
+  if (node < 0 || node >= 64) return;
+  const unsigned long mask = 1ul << node;
+  (void)syscall(SYS_mbind, m, n, 1 /* MPOL_PREFERRED */, &mask, 64UL, 0U);
+}
+
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -126,6 +145,7 @@ struct PinBuf {
       void* m = ::mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
       if (m != MAP_FAILED) {
         (void)::madvise(m, n, MADV_HUGEPAGE);
+        prefer_device_node(m, n);  // before the registration faults the pages in
         if (hipHostRegister(m, n, hipHostRegisterDefault) == hipSuccess) {
           *q = m;
           *len = n;
@@ -1587,10 +1607,12 @@ struct bsg_ctx {
       one(dst, src, n);
       return;
     }
-    const size_t per = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
-    parallel_for((n + per - 1) / per, [=](size_t k) {
-      const size_t o = k * per;
-      one(dst + o, src + o, std::min(per, n - o));
+    // 1 MiB slices taken dynamically, so a thread that wakes late or runs slow takes fewer
+    // (one slice per thread left the others waiting for it)
+    const size_t ns = (n + kCopySlice - 1) / kCopySlice;
+    parallel_for(ns, [=](size_t k) {
+      const size_t o = k * kCopySlice;
+      one(dst + o, src + o, std::min(kCopySlice, n - o));
     });
   }
 

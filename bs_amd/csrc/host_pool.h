@@ -14,6 +14,8 @@ namespace bsg {
 
 // Threads a large copy is split over (BSG_COPY_THREADS, default 8, at most the host's cores).
 int copy_threads();
+// A large copy's unit of work: slices are taken dynamically by the pool's threads.
+constexpr size_t kCopySlice = 1ull << 20;
 
 // Runs fn(i) for every i in [0, n) on the pool and on the calling thread, and returns when all
 // have run. fn must not call parallel_for itself.
