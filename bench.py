@@ -204,26 +204,30 @@ def cpu_full_writer(O, table, host_streams: list, bits: int, min_size: int, thre
 
 
 def chain_roofline(diag: dict) -> dict | None:
-    """k_sha's real bound: the longest chunk's serial SHA-256 chain, run by a skewed octet
-    (sha256_oct_loop.inc: 544 VALU per 64-round block). Two floors: the SIMD's 4 cycles per
-    wave64 VALU instruction, and the instruction-fetch model of DESIGN §4.1 (a lone wave takes
-    in ~1.56 bytes of code per cycle; the loop is 4,308 bytes of VALU code per block). achieved = the
-    in-kernel s_memtime cycles per block of the longest job."""
+    """k_sha's real bound: the longest chunk's serial SHA-256 chain, run by a skewed octet on an
+    early chain (k_early, sha256_oct_solo_loop.inc). Its loop issues 557 instructions per 64-round
+    block (66 iterations of 8 VALU: 64 rounds + the skew's fill and drain; 16 ds_read_b128 of
+    K+W; 4 cndmask, 4 feed-forward adds, 2 waits, 3 loop control), and a lone wave issues one
+    every 4.0 cycles (tools/ubench/oct_pmc under rocprofv3: SQ_ACTIVE_INST_ANY per counted
+    instruction, profiles/r06_oct_pmc.json). Floors: that issue count x 4 (the loop as built),
+    and 64 rounds x 8 VALU x 4 (the octet formulation with no fill, drain or K+W reads).
+    achieved = the in-kernel s_memtime cycles per block of the longest job."""
     try:
         cyc = float(diag["long"]["cycles_per_block"])
     except (KeyError, TypeError, ValueError):
         return None
     if cyc <= 0:
         return None
-    valu = 544
-    floor = valu * 4.0
-    fetch = 4308 / 1.56
-    # the longest chunk runs on an early chain (k_early) when one was picked, else in k_sha
-    return {"bound": "issue / instruction fetch (serial chain)",
+    loop = 557
+    floor = loop * 4.0
+    formulation = 64 * 8 * 4.0
+    return {"bound": "issue (serial chain, lone wave: 4 cycles per instruction)",
             "kernel": "k_early / k_sha wave mode (skewed octet)",
-            "floor_cycles_per_block": floor, "fetch_model_cycles_per_block": round(fetch, 1),
+            "loop_instructions_per_block": loop, "floor_cycles_per_block": floor,
+            "formulation_floor_cycles_per_block": formulation,
             "achieved_cycles_per_block": round(cyc, 1), "frac": round(floor / cyc, 4),
-            "frac_of_fetch_model": round(fetch / cyc, 4), "blocks": diag["long"].get("blocks")}
+            "frac_of_formulation": round(formulation / cyc, 4),
+            "pmc_src": "profiles/r06_oct_pmc.json", "blocks": diag["long"].get("blocks")}
 
 
 def host_placement() -> dict:
