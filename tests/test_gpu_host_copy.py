@@ -56,6 +56,11 @@ def test_stream_stats_reset(gpu):
     w.close()
     a = w.stats()
     assert a["h2d_copies"] >= 1
+    # the stages are placed on the GPU's NUMA node (mbind preferred before registration); the
+    # 20 MiB stream's copy ran as 1 MiB slices, counted by the copying threads' nodes
+    if a["gpu_node"] >= 0 and a["stage_nodes"]:
+        assert a["gpu_node"] in a["stage_nodes"], a
+    assert sum(a["copy_mib_by_node"]) == pytest.approx(20, abs=1), a
     w.reset()
     b = w.stats()
     assert b["h2d_copies"] == 0 and b["host_copy_ms"] == 0 and b["h2d_span_ms"] == 0
