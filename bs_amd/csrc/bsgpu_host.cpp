@@ -40,7 +40,7 @@
 
 using namespace bsg;
 
-int device_node(int device);  // NUMA node of a HIP device (below)
+static int device_node(int device);  // NUMA node of a HIP device (below)
 
 namespace {
 
@@ -908,7 +908,7 @@ constexpr uint64_t kDefaultCarryCap = 8ull << 20;
 // Tiles in flight. Each has its own HIP stream, and streams beyond the process's hardware
 // queues (GPU_MAX_HW_QUEUES, 4 by default) share a queue and serialise behind each other's
 // k_sha, so the default stays below that.
-int default_slots() {
+static int default_slots() {
   const char* e = std::getenv("BSG_STREAM_SLOTS");
   const int v = e ? std::atoi(e) : 3;
   return std::max(2, std::min(kMaxSlots, v));
@@ -920,7 +920,7 @@ int default_slots() {
 // previous tile), only for tile i - ndata's: the copies run back to back on their own stream
 // while the chains of earlier tiles finish.
 constexpr int kMaxData = 8;
-int default_data_slots(int nslots) {
+static int default_data_slots(int nslots) {
   const char* e = std::getenv("BSG_DATA_SLOTS");
   const int v = e ? std::atoi(e) : nslots + 1;
   return std::max(std::max(2, nslots), std::min(kMaxData, v));
@@ -1015,14 +1015,14 @@ struct Stage {
 };
 
 // NUMA node of the page holding p (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR; -1 unknown)
-int page_node(const void* p) {
+static int page_node(const void* p) {
   int node = -1;
   if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, 3UL) != 0) return -1;
   return node;
 }
 
 // NUMA node of a HIP device, from its PCI function in sysfs (-1 unknown)
-int device_node(int device) {
+static int device_node(int device) {
   static std::mutex mu;
   static int cache[64];
   static bool have[64];
@@ -1047,7 +1047,7 @@ int device_node(int device) {
   return node;
 }
 
-uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
+static uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now() - t0).count();
 }
@@ -1088,6 +1088,7 @@ struct bsg_ctx {
   hipEvent_t tail0 = nullptr, tail1 = nullptr;  // the final tile's kernels: start, records out
   bool tail_set = false;
   int slast = -1;              // stage of the latest H2D
+  bool sent = false;           // the stream's first H2D is issued (first_flush())
 
   size_t stage_size() const { return std::min(tile, kStageMax); }
 
@@ -1336,6 +1337,7 @@ struct bsg_ctx {
     HCHECK(hipEventRecord(st.ev, cstream));
     st.inflight = true;
     st.timed = true;
+    sent = true;
     stats.h2d_bytes += sfill;
     stats.h2d_copies++;
     slast = scur;
@@ -1376,6 +1378,15 @@ struct bsg_ctx {
   }
   size_t stage_room() const {
     return std::min(stages[scur].buf.cap, stage_size()) - sfill;
+  }
+  // The stream's first kFirstFlush staged bytes go to the device at once instead of when the
+  // first stage is full, so the H2D pipeline starts a 32 MiB Write earlier (with a full 64 MiB
+  // first stage the copy stream idled until the second Write was copied). Later stages flush
+  // full, as before; not the tile's last bytes (a final segment keeps them, see write()).
+  static constexpr size_t kFirstFlush = 8ull << 20;
+  int first_flush() {
+    if (sent || sfill < kFirstFlush || fill >= tile) return BSG_OK;
+    return flush_stage();
   }
 
   int submit(bool final_seg) {
@@ -1500,6 +1511,7 @@ struct bsg_ctx {
       // here, it is submitted as the final segment
       if (stage_room() == 0 && fill < tile && (rc = flush_stage())) return rc;
     }
+    if (int rc = first_flush()) return rc;
     return poll();
   }
 
@@ -1586,6 +1598,7 @@ struct bsg_ctx {
       int rc = flush_stage();
       if (rc) return rc;
     }
+    if (int rc = first_flush()) return rc;
     return poll();
   }
 
@@ -1648,6 +1661,7 @@ struct bsg_ctx {
     span_set = false;
     tail_set = false;
     slast = -1;
+    sent = false;
     inflight.clear();
     ready.clear();
     cur = 0;
