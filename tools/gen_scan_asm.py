@@ -308,6 +308,7 @@ def main():
 
 
 def write(L, path, name):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
     nvalu = sum(1 for l in L if l.startswith("v_"))
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_scan_asm.py -- do not edit.\n")
