@@ -1816,11 +1816,24 @@ __global__ __launch_bounds__(256) void k_lens(ShaArgs a) {
     }
     a.jinfo[j] = info;
   }
+  // one atomic pair per workgroup, not per wave: the 4,096 waves' same-address atomics cost ~25 us
+  // of the kernel's 57-70 on configs[2] (now 28-40; the launch is one job per thread,
+  // profiles/r06_c16_*)
+  __shared__ uint64_t wmx[4], wtot[4];
   for (int o = 32; o > 0; o >>= 1) {
     mx = max(mx, (uint64_t)__shfl_down(mx, o));
     tot += (uint64_t)__shfl_down(tot, o);
   }
   if ((threadIdx.x & 63) == 0) {
+    wmx[threadIdx.x >> 6] = mx;
+    wtot[threadIdx.x >> 6] = tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      mx = max(mx, wmx[w]);
+      tot += wtot[w];
+    }
     if (mx) atomicMax(reinterpret_cast<unsigned long long*>(&a.ctr->max_nblocks), (unsigned long long)mx);
     if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->total_blocks), (unsigned long long)tot);
   }
