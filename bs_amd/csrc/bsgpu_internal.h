@@ -108,7 +108,7 @@ struct Counters {
   uint64_t lane_end_rt;        // latest s_memrealtime at which a wave left per-lane mode
   uint64_t nlong_grp;          // long jobs on solo / kGroup tickets; the rest of the long list
   uint64_t tickets_grp;        //   runs on pair tickets (kPairGroup jobs, one lane pair each)
-  uint64_t nrefine;            // strips k_scan listed for the exact pass (k_refine)
+  uint64_t nrefine;            // strips k_scan listed for its exact pass
   uint64_t helped;             // solo tickets [0, helped) run with a helper wave (k_sha)
   uint64_t scan_ticket;        // k_scan's strip groups handed out past the first (BSG_SCAN_DYN)
   uint64_t pad[7];

@@ -91,7 +91,7 @@ __device__ __forceinline__ uint32_t lookup(const uint32_t* tab, uint32_t w, uint
   return lds_u32(tab, tab_addr(w, lane4, k));
 }
 
-// Called by kScanWG-thread workgroups only (k_scan, k_refine, k_rescan). 256 rows x 64 replicas;
+// Called by k_scan (kScanThreads) and k_rescan (kScanWG) workgroups. 256 rows x 64 replicas;
 // each uint4 store writes 4 replicas of one row. A thread issues all of its loads before its
 // stores: as a load-store loop, each of the 8 iterations waited for its global load (~8
 // dependent L2 round trips at the start of every workgroup, before any scanning).
@@ -153,8 +153,8 @@ __device__ __forceinline__ void emit(const ScanArgs& a, StripCtx& c, uint64_t st
 // tz <= 32). Loads are whole 64-byte blocks (BSG_READ_SLACK makes the tail block readable).
 // Returns the hash at the last position scanned. FULL (n == 64, every hit block): the lookups of
 // each group of kExactGroup positions are issued together before its steps; with a per-position
-// `k < n` test every step was its own basic block and waited for its own two LDS reads (k_refine
-// ~26 us on 16 K strips).
+// `k < n` test every step was its own basic block and waited for its own two LDS reads (the
+// exact pass, then the k_refine kernel, ~26 us on 16 K strips).
 constexpr int kExactGroup = 8;
 template <bool WRITE, bool FULL>
 __device__ __forceinline__ uint32_t exact_block(const ScanArgs& a, const uint32_t* tab,
@@ -328,7 +328,7 @@ struct StripJob {
   const uint8_t* pre;  // the 64 bytes before the strip (the segment history for its first strip)
   uint64_t start;      // segment offset of the strip
   uint32_t len;        // bytes in the strip
-  bool tail;           // k_refine has the segment's < 64-byte tail or the final flush here
+  bool tail;           // the exact pass has the segment's < 64-byte tail or the final flush here
   bool fin;            // the segment ends its stream (Splitter.Close's flush at its last byte)
   uint64_t seglen;     // the segment's length
 };
