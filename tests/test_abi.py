@@ -30,6 +30,10 @@ def test_struct_layout_and_defaults():
     p = bsgpu.lib().bsg_params_default()
     assert (p.split_bits, p.min_size, p.fanout) == (16, 1024, 8)  # split/split.go:48,88-89
     assert ctypes.sizeof(bsgpu.Params) == 16
+    # bsg_stream_stats (include/bsgpu.h): 13 u64 words (9 counters and copy_bytes_node[4]), then
+    # gpu_node (i32) and three u32 masks/flags
+    assert ctypes.sizeof(bsgpu.StreamStats) == 13 * 8 + 4 * 4
+    assert bsgpu.StreamStats.gpu_node.offset == 13 * 8
 
 
 def test_default_table_matches_golden():
