@@ -712,6 +712,10 @@ def main():
             "sha_path": leg["diag"],
             "chain_roofline": chain_roofline(leg["diag"]),
             "configs2": c2,
+            # how the timed region was run: the library's defaults (no knob set by the bench),
+            # bsg_init first unless BSG_BENCH_INIT=0, Python's cyclic GC off inside timed loops
+            "host_settings": {"library_knobs": "defaults", "bsg_init": init,
+                              "python_gc_in_timed_loops": "off"},
         }
         line["oracle_check"] = leg["check"]
         line["oracle_checked"] = leg["checked"]
